@@ -1,0 +1,186 @@
+/*
+ * dp_mi355x.h -- C ABI of the MI355X-native Depth Pro hot path (libdp_mi355x.so).
+ *
+ * The reference (tdj28/ml-depth-pro-video) has no native code: its hot path
+ * `DepthPro.infer` (src/depth_pro/depth_pro.py:243-298) dispatches PyTorch and
+ * timm ops.  Each entry point below replaces a group of those ops; the comment
+ * on each one cites the reference code it stands in for.  The binding the
+ * reference-side would add (ctypes) is shown in INTEGRATION.md.
+ *
+ * Conventions (all entry points):
+ *   - plain device pointers (HBM), sizes and a HIP stream (hipStream_t passed as
+ *     an opaque pointer; NULL = legacy default stream);
+ *   - no allocation, no host<->device copies, no synchronisation, so every call
+ *     is hipGraph-capturable; the caller owns all buffers;
+ *   - return 0 on success, a hipError_t value (< 1000) if a launch failed, or a
+ *     DP_ERR_* code (>= 1000) for an argument/shape error detected on the host
+ *     before anything was launched;
+ *   - 16-bit tensors are raw bits (uint16) whose kind is given by a DP_BF16 /
+ *     DP_F16 dtype argument; fp32 tensors are `float`.
+ *   - thread-safe for concurrent calls on distinct streams (no global state).
+ */
+#ifndef DP_MI355X_H
+#define DP_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* dp_stream_t;
+
+enum { DP_BF16 = 0, DP_F16 = 1, DP_F32 = 2 };
+enum { DP_OK = 0, DP_ERR_ARG = 1000, DP_ERR_SHAPE = 1001, DP_ERR_ALIGN = 1002, DP_ERR_DTYPE = 1003 };
+enum { DP_ACT_NONE = 0, DP_ACT_RELU = 1, DP_ACT_GELU = 2 };
+enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
+enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1 };
+
+/* ABI version of this header; the Python loader refuses a mismatching .so. */
+#define DP_ABI_VERSION 1
+int dp_abi_version(void);
+
+/*
+ * dp_gemm: C = epilogue(A . B^T), bf16/f16 MFMA (v_mfma_f32_16x16x32_*), fp32 accumulate.
+ *
+ * Replaces every Linear / Conv2d / ConvTranspose2d(k2 s2) of the hot path:
+ *   timm ViT qkv / proj / fc1 / fc2 Linears and the k16 s16 patch-embed conv
+ *     (vit_factory.py:97-99; DINOv2 Block), fov.encoder.1 Linear (fov.py:45-47);
+ *   encoder 1x1 projections + k2s2 deconvs + fuse_lowres (encoder.py:60-130, 314-324);
+ *   decoder 3x3 convs, residual blocks, deconv+out_conv (decoder.py:54-206);
+ *   depth head (depth_pro.py:182-207) and FOV convs (fov.py:28-54, 75-82).
+ *
+ * A operand: DP_A_DENSE  -> A[m][k] row-major, leading dim lda (elements);
+ *            DP_A_CONV   -> implicit im2col of an NHWC tensor [batch][in_h][in_w][in_c]
+ *                           for a k_h x k_w conv (stride, pad) with output out_h x out_w;
+ *                           M = batch*out_h*out_w, K = k_h*k_w*in_c, k = (ky,kx,ci).
+ * B operand: packed weights B[n][k] row-major (ldb), i.e. W for a Linear,
+ *            [Cout][ky][kx][Cin] for a conv, [(dy,dx,Cout)][Cin] for a k2s2 deconv.
+ * Requirements: K % 64 == 0, N % 4 == 0, lda/ldb % 8 == 0, in_c % 64 == 0 (conv).
+ *
+ * Epilogue, per element, in this order:
+ *   v = acc (+ bias[n]) ; act(v) ; (* gamma[n]) ; (+ pos[(m % pos_group) + pos_off][n])
+ *   (+ R1[m][n]) (+ R2[m][n]) ; (+ C[m][n] when accumulate) ; store
+ * Store:   DP_STORE_ROWS      -> C[row(m)][n], row(m) = m, or grouped remap
+ *                                (m / row_group) * row_group_out + row_off + m % row_group;
+ *          DP_STORE_DECONV2X2 -> pixel shuffle: m = (b, y, x) on a dc_h x dc_w grid,
+ *                                n = (dy*2+dx)*dc_cout + co  ->  out pixel (b, 2y+dy, 2x+dx),
+ *                                address C + pixel*ldc + co.
+ * Fused 1x1 head (head_w != NULL; requires N <= 32): out[m] = relu(sum_n v[n]*head_w[n] + head_b)
+ *   written as fp32 to C[m] (the depth head tail, depth_pro.py:200-204).
+ */
+typedef struct dp_gemm_args {
+  int32_t M, N, K;
+  int32_t dtype;            /* DP_BF16 | DP_F16 : element kind of A, B, R1, R2 */
+  const void* A;
+  int64_t lda;
+  const void* B;
+  int64_t ldb;
+  int32_t a_mode;           /* DP_A_DENSE | DP_A_CONV */
+  int32_t relu_a;           /* apply ReLU to A elements as they are loaded */
+  int32_t in_h, in_w, in_c, k_h, k_w, stride, pad, out_h, out_w;  /* conv geometry */
+  const float* bias;        /* [N] or NULL */
+  int32_t act;              /* DP_ACT_* */
+  const float* gamma;       /* [N] or NULL (LayerScale) */
+  const float* pos;         /* fp32 [*][ldpos] or NULL */
+  int64_t ldpos;
+  int32_t pos_group, pos_off;
+  const void* R1;           /* residuals, same element kind, or NULL */
+  int64_t ldr1;
+  const void* R2;
+  int64_t ldr2;
+  void* C;
+  int64_t ldc;
+  int32_t c_dtype;          /* DP_BF16 | DP_F16 | DP_F32 */
+  int32_t accumulate;       /* C += v (fp32 C only) */
+  int32_t store_mode;       /* DP_STORE_* */
+  int32_t dc_h, dc_w, dc_cout;
+  int32_t row_group, row_group_out, row_off;
+  const float* head_w;      /* [N] or NULL */
+  float head_b;
+  int32_t tile;             /* 0 = auto, else a DP_TILE_* hint */
+} dp_gemm_args;
+
+enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32 = 3 };
+
+int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
+
+/*
+ * dp_layernorm: y[r] = LN(x[r]) * w + b over `cols`, fp32 in, 16-bit out.
+ * Replaces timm Block norm1/norm2 and the final `norm` (eps 1e-6).
+ */
+int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy,
+                 int32_t rows, int32_t cols, float eps, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_attention: multi-head softmax attention, flash-style (no S x S in HBM).
+ * qkv: [batch*seq][3*heads*head_dim] (timm's qkv Linear output, (3, heads, hd) column order);
+ * out: [batch*seq][heads*head_dim] (timm's transpose(1,2).reshape). head_dim must be 64.
+ * Replaces timm Attention's F.scaled_dot_product_attention (scale = head_dim^-0.5).
+ */
+int dp_attention(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
+                 int32_t head_dim, float scale, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_normalize_u8: uint8 HWC image -> (x/255 - 0.5)/0.5 planar CHW (fp32 or 16-bit).
+ * Replaces the transform Compose (depth_pro.py:125-132) with the u8 upload + GPU normalize.
+ */
+int dp_normalize_u8(const uint8_t* img_hwc, int32_t H, int32_t W, void* out_chw, int32_t out_dtype,
+                    dp_stream_t stream);
+
+/*
+ * dp_resize_bilinear: planar C x H x W (fp32 or 16-bit) -> C x OH x OW fp32,
+ * bilinear, align_corners=False, no antialias, optional scalar pre-multiply
+ * (F.interpolate as used by DepthPro.infer, depth_pro.py:271-279 and 288-291).
+ */
+int dp_resize_bilinear(const void* src, int32_t src_dtype, int32_t C, int32_t H, int32_t W,
+                       float* dst, int32_t OH, int32_t OW, dp_stream_t stream);
+
+/*
+ * dp_patchify_pyramid: 1536^2 planar fp32 image -> im2col rows of the 35 sliding
+ * windows [35*576][768] (k = c*256 + ky*16 + kx), building the 768^2 and 384^2
+ * pyramid levels on the fly (the bilinear 0.5 / 0.25 resizes are exact 2x2 box
+ * averages).  Replaces _create_pyramid + split + cat (encoder.py:151-188, 245-263)
+ * and the patch-embed unfold.  Window 34 (384^2 level) is also the image-encoder
+ * and FOV-encoder input (encoder.py:308-311, fov.py:66-72).
+ */
+int dp_patchify_pyramid(const float* x0, void* cols, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_vit_cls_rows: x[w*577] = cls + pos[0] for w < n_images (timm _pos_embed cls row),
+ * x fp32 [n_images*577][1024].
+ */
+int dp_vit_cls_rows(float* x, const float* cls, const float* pos, int32_t n_images, dp_stream_t stream);
+
+/*
+ * dp_merge_windows: stitch steps x steps token windows into an NHWC map, dropping the
+ * cls token and cropping `padding` tokens at inner edges (encoder.py:190-231).
+ * src rows: window w token t at row (w*577 + t), ld_src elements, fp32 or 16-bit;
+ * dst: [S][S][1024] 16-bit with S = steps*24 - 2*padding*(steps-1).
+ */
+int dp_merge_windows(const void* src, int32_t src_dtype, int64_t ld_src, int32_t first_window,
+                     int32_t steps, int32_t padding, void* dst, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_fov_tail: final FOV conv 6x6 (32 -> 1) + bias on the 6x6x32 NHWC map
+ * (fov.py:46, head[4]).  w is the PyTorch weight [1][32][6][6] fp32.
+ */
+int dp_fov_tail(const void* x6, int32_t dtype, const float* w, float bias, float* fov_deg,
+                dp_stream_t stream);
+
+/*
+ * dp_infer_epilogue (depth_pro.py:282-298):
+ *   f_px = use_given ? f_given : 0.5*W / tan(0.5*deg2rad(fov_deg))   (fp32)
+ *   inv  = canonical * scale, scale = use_given ? (float)(W / f_given) : W / f_px
+ *   inv  = bilinear(inv, (H, W)) when (H, W) != (1536, 1536)
+ *   depth = 1 / clamp(inv, 1e-4, 1e4)                                  -> depth [H][W] fp32
+ * f_px_out (device float) receives f_px.
+ */
+int dp_infer_epilogue(const float* canonical, int32_t src_h, int32_t src_w, const float* fov_deg,
+                      int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
+                      float* f_px_out, dp_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DP_MI355X_H */

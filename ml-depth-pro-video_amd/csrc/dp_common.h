@@ -1,0 +1,73 @@
+// Shared device helpers for the Depth Pro MI355X (gfx950 / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dp_mi355x.h"
+
+typedef uint16_t u16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+typedef __attribute__((ext_vector_type(2))) short i16x2_t;
+
+// 16-bit element kinds.  Activations and weights are carried as raw u16 bits;
+// the kind only decides the MFMA opcode and the float<->16-bit conversions.
+struct KBF16 {
+  static constexpr int id = DP_BF16;
+  static __device__ __forceinline__ float to_f(u16 v) {
+    return __uint_as_float(((uint32_t)v) << 16);
+  }
+  static __device__ __forceinline__ u16 from_f(float f) {
+    return __builtin_bit_cast(u16, (__bf16)f);
+  }
+  static __device__ __forceinline__ f32x4_t mfma16(uint4 a, uint4 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                   __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x16_t mfma32(uint4 a, uint4 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                   __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+  }
+};
+
+struct KF16 {
+  static constexpr int id = DP_F16;
+  static __device__ __forceinline__ float to_f(u16 v) {
+    return (float)__builtin_bit_cast(_Float16, v);
+  }
+  static __device__ __forceinline__ u16 from_f(float f) {
+    return __builtin_bit_cast(u16, (_Float16)f);
+  }
+  static __device__ __forceinline__ f32x4_t mfma16(uint4 a, uint4 b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a),
+                                                  __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x16_t mfma32(uint4 a, uint4 b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a),
+                                                  __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  }
+};
+
+// ReLU on packed 16-bit floats (bf16 or f16): a negative value has its sign bit
+// set, i.e. is a negative int16, so max_i16(x, 0) zeroes it (-0 and negative
+// NaNs included) and leaves every non-negative value bit-identical.
+__device__ __forceinline__ uint32_t relu_pk16(uint32_t v) {
+  i16x2_t x = __builtin_bit_cast(i16x2_t, v);
+  i16x2_t z = {0, 0};
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, z));
+}
+__device__ __forceinline__ uint4 relu_pk16(uint4 v) {
+  return make_uint4(relu_pk16(v.x), relu_pk16(v.y), relu_pk16(v.z), relu_pk16(v.w));
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+#define DP_CHECK_LAUNCH()                                        \
+  do {                                                           \
+    hipError_t e__ = hipGetLastError();                          \
+    if (e__ != hipSuccess) return (int)e__;                      \
+  } while (0)

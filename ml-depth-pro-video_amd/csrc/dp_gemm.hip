@@ -1,0 +1,341 @@
+// dp_gemm: LDS-tiled bf16/f16 MFMA GEMM with an implicit-conv A loader and a
+// fused epilogue, for gfx950 (CDNA4).
+//
+// Tile: BM x BN x 64, 256 threads = 4 wave64s laid out WM x WN; each wave owns
+// a (BM/WM) x (BN/WN) sub-tile of 16x16 fragments computed with
+// v_mfma_f32_16x16x32_{bf16,f16}.  Operands are staged global -> VGPR -> LDS
+// (double-buffered, one barrier per K-tile); LDS rows are 128 B with the
+// chunk index XOR-swizzled by (row & 7) so the ds_read_b128 fragment reads are
+// bank-conflict free.  The MFMA is issued with the weight fragment as the
+// A-operand and the activation fragment as the B-operand, so D = C^T: every
+// lane ends up with 4 consecutive output channels of one output row, which
+// makes bias/gamma loads and the stores 8-16 B wide.
+#include "dp_common.h"
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int NT = 256;
+
+struct GemmP {
+  int M, N, K;
+  const u16* A;
+  long long lda;
+  const u16* B;
+  long long ldb;
+  int relu_a;
+  int in_h, in_w, in_c, k_w, stride, pad, out_h, out_w;
+  const float* bias;
+  int act;
+  const float* gamma;
+  const float* pos;
+  long long ldpos;
+  int pos_group, pos_off;
+  const u16* R1;
+  long long ldr1;
+  const u16* R2;
+  long long ldr2;
+  void* C;
+  long long ldc;
+  int c_dtype;
+  int accumulate;
+  int store_mode;
+  int dc_h, dc_w, dc_cout;
+  int row_group, row_group_out, row_off;
+  const float* head_w;
+  float head_b;
+  int tiles_n;
+};
+
+__device__ __forceinline__ int lds_off(int row, int chunk) {
+  return row * BK + ((chunk ^ (row & 7)) << 3);
+}
+
+template <typename K_, int BM, int BN, int WM, int WN, bool CONV>
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int CA = BM * 8 / NT;  // 16-B chunks per thread per A tile
+  constexpr int CB = BN * 8 / NT;
+  static_assert(CA >= 1 && CB >= 1 && WM * WN == 4, "tile config");
+  __shared__ __attribute__((aligned(16))) u16 smem[2][(BM + BN) * BK];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int tile_n = blockIdx.x % p.tiles_n;
+  const int tile_m = blockIdx.x / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kc = tid & 7;        // 16-B chunk within a 64-wide K row
+  const int rbase = tid >> 3;    // first row of this thread's chunks (step 32)
+
+  // ---- per-thread load descriptors
+  const u16* a_ptr[CA];
+  int a_iy[CA], a_ix[CA], a_pix[CA];
+  #pragma unroll
+  for (int i = 0; i < CA; ++i) {
+    int m = m0 + rbase + 32 * i;
+    bool ok = m < p.M;
+    int mc = ok ? m : p.M - 1;
+    if constexpr (!CONV) {
+      a_ptr[i] = p.A + (long long)mc * p.lda + kc * 8;
+    } else {
+      int hw = p.out_h * p.out_w;
+      int b = mc / hw, r = mc - b * hw;
+      int oy = r / p.out_w, ox = r - oy * p.out_w;
+      a_iy[i] = ok ? oy * p.stride - p.pad : -(1 << 28);
+      a_ix[i] = ox * p.stride - p.pad;
+      a_pix[i] = b * p.in_h * p.in_w;
+    }
+  }
+  const u16* b_ptr[CB];
+  #pragma unroll
+  for (int i = 0; i < CB; ++i) {
+    int n = n0 + rbase + 32 * i;
+    n = n < p.N ? n : p.N - 1;
+    b_ptr[i] = p.B + (long long)n * p.ldb + kc * 8;
+  }
+
+  uint4 ra[CA], rb[CB];
+  // conv tap state (uniform): current (ky, kx, ci0) of the K tile being loaded
+  int t_ky = 0, t_kx = 0, t_ci = 0;
+
+  auto load_tile = [&](int k0) {
+    if constexpr (!CONV) {
+      #pragma unroll
+      for (int i = 0; i < CA; ++i) ra[i] = *(const uint4*)(a_ptr[i] + k0);
+    } else {
+      #pragma unroll
+      for (int i = 0; i < CA; ++i) {
+        int iy = a_iy[i] + t_ky, ix = a_ix[i] + t_kx;
+        bool inb = (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (inb) {
+          long long pix = (long long)a_pix[i] + (long long)iy * p.in_w + ix;
+          v = *(const uint4*)(p.A + pix * p.in_c + t_ci + kc * 8);
+        }
+        ra[i] = v;
+      }
+      t_ci += BK;
+      if (t_ci == p.in_c) {
+        t_ci = 0;
+        if (++t_kx == p.k_w) { t_kx = 0; ++t_ky; }
+      }
+    }
+    #pragma unroll
+    for (int i = 0; i < CB; ++i) rb[i] = *(const uint4*)(b_ptr[i] + k0);
+  };
+  auto store_tile = [&](int buf) {
+    u16* sa = smem[buf];
+    u16* sb = smem[buf] + BM * BK;
+    #pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      uint4 v = ra[i];
+      if (p.relu_a) v = relu_pk16(v);
+      *(uint4*)(sa + lds_off(rbase + 32 * i, kc)) = v;
+    }
+    #pragma unroll
+    for (int i = 0; i < CB; ++i) *(uint4*)(sb + lds_off(rbase + 32 * i, kc)) = rb[i];
+  };
+
+  f32x4_t acc[FM][FN];
+  #pragma unroll
+  for (int i = 0; i < FM; ++i)
+    #pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = p.K / BK;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  const int frow = lane & 15;
+  const int fchunk = lane >> 4;
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_tile((kt + 1) * BK);
+    const u16* sa = smem[cur];
+    const u16* sb = smem[cur] + BM * BK;
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 af[FM], bf[FN];
+      #pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *(const uint4*)(sa + lds_off(wm * TM + i * 16 + frow, ks * 4 + fchunk));
+      #pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bf[j] = *(const uint4*)(sb + lds_off(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      #pragma unroll
+      for (int i = 0; i < FM; ++i)
+        #pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af[i], acc[i][j]);
+    }
+    if (kt + 1 < KT) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds rows m = .. + (lane & 15), cols n = .. + 4*(lane >> 4) + r
+  const int em = lane & 15;
+  const int en = 4 * (lane >> 4);
+  float hsum[FM];
+  #pragma unroll
+  for (int i = 0; i < FM; ++i) hsum[i] = 0.f;
+
+  #pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * TM + i * 16 + em;
+    #pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * TN + j * 16 + en;
+      if (m >= p.M || n >= p.N) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (p.bias) {
+        float4 b = *(const float4*)(p.bias + n);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (p.act == DP_ACT_RELU) {
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      } else if (p.act == DP_ACT_GELU) {
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+      }
+      if (p.gamma) {
+        float4 g = *(const float4*)(p.gamma + n);
+        v[0] *= g.x; v[1] *= g.y; v[2] *= g.z; v[3] *= g.w;
+      }
+      if (p.pos) {
+        const float* pp = p.pos + (long long)(m % p.pos_group + p.pos_off) * p.ldpos + n;
+        float4 q = *(const float4*)pp;
+        v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+      }
+      if (p.R1) {
+        uint2 r = *(const uint2*)(p.R1 + (long long)m * p.ldr1 + n);
+        v[0] += K_::to_f(r.x & 0xffff); v[1] += K_::to_f(r.x >> 16);
+        v[2] += K_::to_f(r.y & 0xffff); v[3] += K_::to_f(r.y >> 16);
+      }
+      if (p.R2) {
+        uint2 r = *(const uint2*)(p.R2 + (long long)m * p.ldr2 + n);
+        v[0] += K_::to_f(r.x & 0xffff); v[1] += K_::to_f(r.x >> 16);
+        v[2] += K_::to_f(r.y & 0xffff); v[3] += K_::to_f(r.y >> 16);
+      }
+      if (p.head_w) {
+        float4 w = *(const float4*)(p.head_w + n);
+        hsum[i] += v[0] * w.x + v[1] * w.y + v[2] * w.z + v[3] * w.w;
+        continue;
+      }
+      long long off;
+      if (p.store_mode == DP_STORE_DECONV2X2) {
+        const int hw = p.dc_h * p.dc_w;
+        const int b = m / hw, rr = m - b * hw;
+        const int y = rr / p.dc_w, x = rr - y * p.dc_w;
+        const int q = n / p.dc_cout, co = n - q * p.dc_cout;
+        const long long pix = ((long long)b * 2 * p.dc_h + 2 * y + (q >> 1)) * (2 * p.dc_w) + 2 * x + (q & 1);
+        off = pix * p.ldc + co;
+      } else {
+        long long row = m;
+        if (p.row_group) row = (long long)(m / p.row_group) * p.row_group_out + p.row_off + m % p.row_group;
+        off = row * p.ldc + n;
+      }
+      if (p.c_dtype == DP_F32) {
+        float* c = (float*)p.C + off;
+        if (p.accumulate) {
+          float4 o = *(const float4*)c;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2 o;
+        o.x = (uint32_t)K_::from_f(v[0]) | ((uint32_t)K_::from_f(v[1]) << 16);
+        o.y = (uint32_t)K_::from_f(v[2]) | ((uint32_t)K_::from_f(v[3]) << 16);
+        *(uint2*)((u16*)p.C + off) = o;
+      }
+    }
+  }
+  if (p.head_w) {
+    // a row's channels live in lanes (lane&15) + 16*{0..3} of the wave (WN == 1)
+    #pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      float s = hsum[i];
+      s += __shfl_xor(s, 16);
+      s += __shfl_xor(s, 32);
+      const int m = m0 + wm * TM + i * 16 + em;
+      if ((lane >> 4) == 0 && m < p.M) ((float*)p.C)[m] = fmaxf(s + p.head_b, 0.f);
+    }
+  }
+}
+
+template <typename K_, int BM, int BN, int WM, int WN>
+int launch_t(const GemmP& p0, bool conv, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_m = (p.M + BM - 1) / BM;
+  dim3 grid(p.tiles_n * tiles_m);
+  if (conv)
+    hipLaunchKernelGGL((gemm_kernel<K_, BM, BN, WM, WN, true>), grid, dim3(NT), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_kernel<K_, BM, BN, WM, WN, false>), grid, dim3(NT), 0, s, p);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename K_>
+int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
+  switch (tile) {
+    case DP_TILE_256x64: return launch_t<K_, 256, 64, 4, 1>(p, conv, s);
+    case DP_TILE_256x32: return launch_t<K_, 256, 32, 4, 1>(p, conv, s);
+    default: return launch_t<K_, 128, 128, 2, 2>(p, conv, s);
+  }
+}
+
+}  // namespace
+
+extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
+  if (!a) return DP_ERR_ARG;
+  if (a->M <= 0 || a->N <= 0 || a->K <= 0) return DP_ERR_SHAPE;
+  if (a->K % BK != 0 || a->N % 4 != 0) return DP_ERR_SHAPE;
+  if (a->ldb % 8 != 0 || (a->a_mode == DP_A_DENSE && a->lda % 8 != 0)) return DP_ERR_ALIGN;
+  if (!a->A || !a->B || !a->C) return DP_ERR_ARG;
+  if (a->dtype != DP_BF16 && a->dtype != DP_F16) return DP_ERR_DTYPE;
+  if (a->c_dtype != DP_BF16 && a->c_dtype != DP_F16 && a->c_dtype != DP_F32) return DP_ERR_DTYPE;
+  if (a->c_dtype != DP_F32 && a->c_dtype != a->dtype) return DP_ERR_DTYPE;
+  if (a->accumulate && a->c_dtype != DP_F32) return DP_ERR_DTYPE;
+  if (a->pos && (a->pos_group <= 0)) return DP_ERR_ARG;
+  if (a->a_mode == DP_A_CONV) {
+    if (a->in_c % BK != 0 || a->k_h * a->k_w * a->in_c != a->K) return DP_ERR_SHAPE;
+    if (a->out_h <= 0 || a->out_w <= 0 || a->stride <= 0 || a->M % (a->out_h * a->out_w) != 0)
+      return DP_ERR_SHAPE;
+  }
+  if (a->store_mode == DP_STORE_DECONV2X2) {
+    if (a->dc_cout % 4 != 0 || a->N != 4 * a->dc_cout || a->dc_h <= 0 || a->dc_w <= 0 ||
+        a->M % (a->dc_h * a->dc_w) != 0)
+      return DP_ERR_SHAPE;
+  }
+  int tile = a->tile;
+  if (a->head_w) {
+    if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;
+    tile = DP_TILE_256x32;
+  }
+  if (tile == DP_TILE_AUTO) tile = a->N <= 32 ? DP_TILE_256x32 : (a->N <= 64 ? DP_TILE_256x64 : DP_TILE_128x128);
+
+  GemmP p;
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.A = (const u16*)a->A; p.lda = a->lda;
+  p.B = (const u16*)a->B; p.ldb = a->ldb;
+  p.relu_a = a->relu_a;
+  p.in_h = a->in_h; p.in_w = a->in_w; p.in_c = a->in_c; p.k_w = a->k_w;
+  p.stride = a->stride; p.pad = a->pad; p.out_h = a->out_h; p.out_w = a->out_w;
+  p.bias = a->bias; p.act = a->act; p.gamma = a->gamma;
+  p.pos = a->pos; p.ldpos = a->ldpos; p.pos_group = a->pos_group; p.pos_off = a->pos_off;
+  p.R1 = (const u16*)a->R1; p.ldr1 = a->ldr1; p.R2 = (const u16*)a->R2; p.ldr2 = a->ldr2;
+  p.C = a->C; p.ldc = a->ldc; p.c_dtype = a->c_dtype; p.accumulate = a->accumulate;
+  p.store_mode = a->store_mode; p.dc_h = a->dc_h; p.dc_w = a->dc_w; p.dc_cout = a->dc_cout;
+  p.row_group = a->row_group; p.row_group_out = a->row_group_out; p.row_off = a->row_off;
+  p.head_w = a->head_w; p.head_b = a->head_b;
+  p.tiles_n = 1;
+  hipStream_t s = (hipStream_t)stream;
+  const bool conv = a->a_mode == DP_A_CONV;
+  if (a->dtype == DP_BF16) return launch_k<KBF16>(p, tile, conv, s);
+  return launch_k<KF16>(p, tile, conv, s);
+}

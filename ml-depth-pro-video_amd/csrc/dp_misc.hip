@@ -1,0 +1,393 @@
+// HBM-bound helper kernels of the Depth Pro hot path (gfx950): LayerNorm,
+// input normalisation, bilinear resize, fused pyramid + window im2col, cls
+// rows, window merge, FOV tail, infer epilogue.  All loads/stores are 16 B per
+// lane where the layout allows (coalesced), one pass over HBM each.
+#include "dp_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------ LayerNorm
+// One wave64 per row, the row held in registers (VEC float4 per lane), two-pass
+// mean / variance in fp32 (timm nn.LayerNorm(eps=1e-6)), 16-bit output.
+template <typename K_, int VEC>
+__global__ void __launch_bounds__(256) ln_kernel(const float* __restrict__ x, long long ldx,
+                                                 const float* __restrict__ w, const float* __restrict__ b,
+                                                 u16* __restrict__ y, long long ldy, int rows, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int COLS = VEC * 256;
+  const float* xr = x + (long long)row * ldx;
+  float4 v[VEC];
+  float s = 0.f;
+  #pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    v[i] = *(const float4*)(xr + i * 256 + lane * 4);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  #pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s * (1.f / COLS);
+  float q = 0.f;
+  #pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    float a = v[i].x - mean, bb = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+    q += (a * a + bb * bb) + (c * c + d * d);
+  }
+  #pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = rsqrtf(q * (1.f / COLS) + eps);
+  u16* yr = y + (long long)row * ldy;
+  #pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int c0 = i * 256 + lane * 4;
+    float4 g = *(const float4*)(w + c0);
+    float4 bb = *(const float4*)(b + c0);
+    float o0 = (v[i].x - mean) * rstd * g.x + bb.x;
+    float o1 = (v[i].y - mean) * rstd * g.y + bb.y;
+    float o2 = (v[i].z - mean) * rstd * g.z + bb.z;
+    float o3 = (v[i].w - mean) * rstd * g.w + bb.w;
+    uint2 pk;
+    pk.x = (uint32_t)K_::from_f(o0) | ((uint32_t)K_::from_f(o1) << 16);
+    pk.y = (uint32_t)K_::from_f(o2) | ((uint32_t)K_::from_f(o3) << 16);
+    *(uint2*)(yr + c0) = pk;
+  }
+}
+
+template <typename K_>
+int ln_launch(const float* x, long long ldx, const float* w, const float* b, u16* y, long long ldy,
+              int rows, int cols, float eps, hipStream_t s) {
+  dim3 grid((rows + 3) / 4);
+  switch (cols) {
+    case 256: hipLaunchKernelGGL((ln_kernel<K_, 1>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
+    case 512: hipLaunchKernelGGL((ln_kernel<K_, 2>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
+    case 1024: hipLaunchKernelGGL((ln_kernel<K_, 4>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
+    case 2048: hipLaunchKernelGGL((ln_kernel<K_, 8>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
+    default: return DP_ERR_SHAPE;
+  }
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+// --------------------------------------------------------- u8 HWC -> CHW norm
+template <int OUT>
+__global__ void normalize_kernel(const uint8_t* __restrict__ img, int HW, void* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= HW) return;
+  #pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    // ToTensor: u8 / 255 (fp32), Normalize: (x - 0.5) / 0.5
+    float v = ((float)img[3 * i + c] / 255.0f - 0.5f) / 0.5f;
+    if constexpr (OUT == DP_F32) ((float*)out)[(long long)c * HW + i] = v;
+    else if constexpr (OUT == DP_BF16) ((u16*)out)[(long long)c * HW + i] = KBF16::from_f(v);
+    else ((u16*)out)[(long long)c * HW + i] = KF16::from_f(v);
+  }
+}
+
+// ------------------------------------------------------------ bilinear resize
+// PyTorch upsample_bilinear2d, align_corners=False, explicit output size:
+// scale = in/out, src = max(scale*(dst+0.5)-0.5, 0), h1 = h0 + (h0 < in-1).
+__device__ __forceinline__ void src_index(int d, float scale, int in, int& i0, int& i1, float& l0, float& l1) {
+  float s = scale * ((float)d + 0.5f) - 0.5f;
+  s = s < 0.f ? 0.f : s;
+  i0 = (int)s;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+  l0 = 1.f - l1;
+}
+
+template <int SRC>
+__device__ __forceinline__ float ld_any(const void* p, long long i) {
+  if constexpr (SRC == DP_F32) return ((const float*)p)[i];
+  else if constexpr (SRC == DP_BF16) return KBF16::to_f(((const u16*)p)[i]);
+  else return KF16::to_f(((const u16*)p)[i]);
+}
+
+template <int SRC>
+__global__ void resize_kernel(const void* __restrict__ src, int C, int H, int W, float* __restrict__ dst,
+                              int OH, int OW, float sh, float sw) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)C * OH * OW;
+  if (i >= total) return;
+  const int ox = i % OW;
+  const int oy = (i / OW) % OH;
+  const int c = i / ((long long)OW * OH);
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  src_index(oy, sh, H, y0, y1, ly0, ly1);
+  src_index(ox, sw, W, x0, x1, lx0, lx1);
+  const long long pb = (long long)c * H * W;
+  const float v00 = ld_any<SRC>(src, pb + (long long)y0 * W + x0);
+  const float v01 = ld_any<SRC>(src, pb + (long long)y0 * W + x1);
+  const float v10 = ld_any<SRC>(src, pb + (long long)y1 * W + x0);
+  const float v11 = ld_any<SRC>(src, pb + (long long)y1 * W + x1);
+  dst[i] = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+}
+
+// ------------------------------------------- pyramid + sliding windows + im2col
+// Row m = w*576 + py*24 + px (window w, token), col k = c*256 + ky*16 + kx.
+// Windows 0..24: 1536^2 level, stride 288; 25..33: 768^2 level, stride 192;
+// 34: 384^2 level (encoder.py:170-188, 253-263).  The 0.5 / 0.25 bilinear
+// resizes (encoder.py:151-168) are exactly 2-tap averages per axis (taps
+// {2d, 2d+1} and {4d+1, 4d+2}); they are evaluated in PyTorch's order
+// 0.5*(0.5*a + 0.5*b) + 0.5*(0.5*c + 0.5*d).
+template <typename K_>
+__global__ void patchify_kernel(const float* __restrict__ x0, u16* __restrict__ cols) {
+  const int S = 1536;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // (m, c, ky)
+  const int total = 35 * 576 * 48;
+  if (i >= total) return;
+  const int ky = i % 16;
+  const int c = (i / 16) % 3;
+  const int m = i / 48;
+  const int w = m / 576, t = m % 576;
+  const int py = t / 24, px = t % 24;
+  const float* plane = x0 + (long long)c * S * S;
+  float v[16];
+  if (w < 25) {
+    const int oy = (w / 5) * 288, ox = (w % 5) * 288;
+    const float* r = plane + (long long)(oy + py * 16 + ky) * S + ox + px * 16;
+    #pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 f = *(const float4*)(r + 4 * q);
+      v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+    }
+  } else if (w < 34) {
+    const int ww = w - 25;
+    const int Y = (ww / 3) * 192 + py * 16 + ky, X0 = (ww % 3) * 192 + px * 16;
+    const float* r0 = plane + (long long)(2 * Y) * S + 2 * X0;
+    const float* r1 = r0 + S;
+    #pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float4 a = *(const float4*)(r0 + 4 * q);
+      float4 b = *(const float4*)(r1 + 4 * q);
+      v[2 * q] = 0.5f * (0.5f * a.x + 0.5f * a.y) + 0.5f * (0.5f * b.x + 0.5f * b.y);
+      v[2 * q + 1] = 0.5f * (0.5f * a.z + 0.5f * a.w) + 0.5f * (0.5f * b.z + 0.5f * b.w);
+    }
+  } else {
+    const int Y = py * 16 + ky, X0 = px * 16;
+    const float* r0 = plane + (long long)(4 * Y + 1) * S + 4 * X0;
+    const float* r1 = r0 + S;
+    #pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float4 a = *(const float4*)(r0 + 4 * q);
+      float4 b = *(const float4*)(r1 + 4 * q);
+      // taps 4X+1, 4X+2 of rows 4Y+1, 4Y+2
+      v[q] = 0.5f * (0.5f * a.y + 0.5f * a.z) + 0.5f * (0.5f * b.y + 0.5f * b.z);
+    }
+  }
+  uint32_t pk[8];
+  #pragma unroll
+  for (int q = 0; q < 8; ++q) pk[q] = (uint32_t)K_::from_f(v[2 * q]) | ((uint32_t)K_::from_f(v[2 * q + 1]) << 16);
+  u16* dst = cols + (long long)m * 768 + c * 256 + ky * 16;
+  *(uint4*)dst = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  *(uint4*)(dst + 8) = make_uint4(pk[4], pk[5], pk[6], pk[7]);
+}
+
+__global__ void cls_kernel(float* __restrict__ x, const float* __restrict__ cls, const float* __restrict__ pos, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * 1024) return;
+  const int w = i / 1024, c = i % 1024;
+  x[(long long)w * 577 * 1024 + c] = cls[c] + pos[c];
+}
+
+// ------------------------------------------------------------- window merge
+__device__ __forceinline__ void merge_axis(int Y, int steps, int pad, int& j, int& yy) {
+  if (steps == 1) { j = 0; yy = Y; return; }
+  const int first = 24 - pad, mid = 24 - 2 * pad;
+  if (Y < first) { j = 0; yy = Y; return; }
+  const int y2 = Y - first;
+  j = 1 + y2 / mid;
+  if (j > steps - 1) j = steps - 1;
+  yy = pad + (y2 - (j - 1) * mid);
+}
+
+template <typename K_, int SRC>
+__global__ void merge_kernel(const void* __restrict__ src, long long ld, int w0, int steps, int pad, int S,
+                             u16* __restrict__ dst) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (pixel, 8-channel group)
+  if (i >= (long long)S * S * 128) return;
+  const int g = i % 128;
+  const int pix = i / 128;
+  const int Y = pix / S, X = pix % S;
+  int j, yy, ii, xx;
+  merge_axis(Y, steps, pad, j, yy);
+  merge_axis(X, steps, pad, ii, xx);
+  const long long row = (long long)(w0 + j * steps + ii) * 577 + 1 + yy * 24 + xx;
+  uint32_t pk[4];
+  if constexpr (SRC == DP_F32) {
+    const float* s = (const float*)src + row * ld + g * 8;
+    float4 a = *(const float4*)s, b = *(const float4*)(s + 4);
+    pk[0] = (uint32_t)K_::from_f(a.x) | ((uint32_t)K_::from_f(a.y) << 16);
+    pk[1] = (uint32_t)K_::from_f(a.z) | ((uint32_t)K_::from_f(a.w) << 16);
+    pk[2] = (uint32_t)K_::from_f(b.x) | ((uint32_t)K_::from_f(b.y) << 16);
+    pk[3] = (uint32_t)K_::from_f(b.z) | ((uint32_t)K_::from_f(b.w) << 16);
+  } else {
+    uint4 a = *(const uint4*)((const u16*)src + row * ld + g * 8);
+    pk[0] = a.x; pk[1] = a.y; pk[2] = a.z; pk[3] = a.w;
+  }
+  *(uint4*)(dst + (long long)pix * 1024 + g * 8) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+}
+
+// ------------------------------------------------------------------ FOV tail
+template <typename K_>
+__global__ void fov_tail_kernel(const u16* __restrict__ x6, const float* __restrict__ w, float bias,
+                                float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < 1152; i += 256) {
+    const int ci = i % 32, tap = i / 32;  // x6 NHWC: (ky*6+kx)*32 + ci
+    s += K_::to_f(x6[i]) * w[ci * 36 + tap];
+  }
+  #pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]) + bias;
+}
+
+// ------------------------------------------------------------ infer epilogue
+__global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW, const float* __restrict__ fov,
+                                 int use_given, float given_scale, float given_fpx, int H, int W,
+                                 float* __restrict__ depth, float* __restrict__ fpx_out) {
+  float fpx, scale;
+  if (use_given) {
+    fpx = given_fpx;
+    scale = given_scale;
+  } else {
+    const float deg = fov[0];
+    const float rad = deg * 0.017453292519943295f;  // torch.deg2rad
+    fpx = (0.5f * (float)W) / tanf(0.5f * rad);
+    scale = (float)W / fpx;
+  }
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && fpx_out) fpx_out[0] = fpx;
+  if (i >= (long long)H * W) return;
+  float v;
+  if (H == SH && W == SW) {
+    v = canon[i] * scale;
+  } else {
+    const int ox = i % W, oy = i / W;
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    src_index(oy, (float)SH / (float)H, SH, y0, y1, ly0, ly1);
+    src_index(ox, (float)SW / (float)W, SW, x0, x1, lx0, lx1);
+    const float v00 = canon[(long long)y0 * SW + x0] * scale, v01 = canon[(long long)y0 * SW + x1] * scale;
+    const float v10 = canon[(long long)y1 * SW + x0] * scale, v11 = canon[(long long)y1 * SW + x1] * scale;
+    v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+  }
+  v = fminf(fmaxf(v, 1e-4f), 1e4f);
+  depth[i] = 1.0f / v;
+}
+
+inline int blocks_for(long long n, int bs) { return (int)((n + bs - 1) / bs); }
+
+}  // namespace
+
+extern "C" int dp_abi_version(void) { return DP_ABI_VERSION; }
+
+extern "C" int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy,
+                            int32_t rows, int32_t cols, float eps, int32_t dtype, dp_stream_t stream) {
+  if (!x || !w || !b || !y) return DP_ERR_ARG;
+  if (rows <= 0 || ldx % 4 || ldy % 4) return DP_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DP_BF16) return ln_launch<KBF16>(x, ldx, w, b, (u16*)y, ldy, rows, cols, eps, s);
+  if (dtype == DP_F16) return ln_launch<KF16>(x, ldx, w, b, (u16*)y, ldy, rows, cols, eps, s);
+  return DP_ERR_DTYPE;
+}
+
+extern "C" int dp_normalize_u8(const uint8_t* img, int32_t H, int32_t W, void* out, int32_t out_dtype,
+                               dp_stream_t stream) {
+  if (!img || !out) return DP_ERR_ARG;
+  if (H <= 0 || W <= 0) return DP_ERR_SHAPE;
+  const int HW = H * W;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g(blocks_for(HW, 256));
+  if (out_dtype == DP_F32) hipLaunchKernelGGL(normalize_kernel<DP_F32>, g, dim3(256), 0, s, img, HW, out);
+  else if (out_dtype == DP_BF16) hipLaunchKernelGGL(normalize_kernel<DP_BF16>, g, dim3(256), 0, s, img, HW, out);
+  else if (out_dtype == DP_F16) hipLaunchKernelGGL(normalize_kernel<DP_F16>, g, dim3(256), 0, s, img, HW, out);
+  else return DP_ERR_DTYPE;
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dp_resize_bilinear(const void* src, int32_t src_dtype, int32_t C, int32_t H, int32_t W, float* dst,
+                                  int32_t OH, int32_t OW, dp_stream_t stream) {
+  if (!src || !dst) return DP_ERR_ARG;
+  if (C <= 0 || H <= 0 || W <= 0 || OH <= 0 || OW <= 0) return DP_ERR_SHAPE;
+  const long long total = (long long)C * OH * OW;
+  const float sh = (float)H / (float)OH, sw = (float)W / (float)OW;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g(blocks_for(total, 256));
+  if (src_dtype == DP_F32) hipLaunchKernelGGL(resize_kernel<DP_F32>, g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw);
+  else if (src_dtype == DP_BF16) hipLaunchKernelGGL(resize_kernel<DP_BF16>, g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw);
+  else if (src_dtype == DP_F16) hipLaunchKernelGGL(resize_kernel<DP_F16>, g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw);
+  else return DP_ERR_DTYPE;
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dp_patchify_pyramid(const float* x0, void* cols, int32_t dtype, dp_stream_t stream) {
+  if (!x0 || !cols) return DP_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g(blocks_for(35 * 576 * 48, 256));
+  if (dtype == DP_BF16) hipLaunchKernelGGL(patchify_kernel<KBF16>, g, dim3(256), 0, s, x0, (u16*)cols);
+  else if (dtype == DP_F16) hipLaunchKernelGGL(patchify_kernel<KF16>, g, dim3(256), 0, s, x0, (u16*)cols);
+  else return DP_ERR_DTYPE;
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dp_vit_cls_rows(float* x, const float* cls, const float* pos, int32_t n, dp_stream_t stream) {
+  if (!x || !cls || !pos) return DP_ERR_ARG;
+  if (n <= 0) return DP_ERR_SHAPE;
+  hipLaunchKernelGGL(cls_kernel, dim3(blocks_for(n * 1024, 256)), dim3(256), 0, (hipStream_t)stream, x, cls, pos, n);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dp_merge_windows(const void* src, int32_t src_dtype, int64_t ld, int32_t w0, int32_t steps,
+                                int32_t pad, void* dst, int32_t dtype, dp_stream_t stream) {
+  if (!src || !dst) return DP_ERR_ARG;
+  if (steps <= 0 || pad < 0 || (steps > 1 && 24 - 2 * pad <= 0) || ld % 8) return DP_ERR_SHAPE;
+  const int S = steps == 1 ? 24 : 2 * (24 - pad) + (steps - 2) * (24 - 2 * pad);
+  const long long total = (long long)S * S * 128;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 g(blocks_for(total, 256));
+  if (src_dtype != DP_F32 && src_dtype != dtype) return DP_ERR_DTYPE;
+  if (dtype == DP_BF16) {
+    if (src_dtype == DP_F32) hipLaunchKernelGGL((merge_kernel<KBF16, DP_F32>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
+    else hipLaunchKernelGGL((merge_kernel<KBF16, DP_BF16>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
+  } else if (dtype == DP_F16) {
+    if (src_dtype == DP_F32) hipLaunchKernelGGL((merge_kernel<KF16, DP_F32>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
+    else hipLaunchKernelGGL((merge_kernel<KF16, DP_F16>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
+  } else {
+    return DP_ERR_DTYPE;
+  }
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dp_fov_tail(const void* x6, int32_t dtype, const float* w, float bias, float* fov_deg,
+                           dp_stream_t stream) {
+  if (!x6 || !w || !fov_deg) return DP_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DP_BF16) hipLaunchKernelGGL(fov_tail_kernel<KBF16>, dim3(1), dim3(256), 0, s, (const u16*)x6, w, bias, fov_deg);
+  else if (dtype == DP_F16) hipLaunchKernelGGL(fov_tail_kernel<KF16>, dim3(1), dim3(256), 0, s, (const u16*)x6, w, bias, fov_deg);
+  else return DP_ERR_DTYPE;
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dp_infer_epilogue(const float* canonical, int32_t SH, int32_t SW, const float* fov_deg,
+                                 int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
+                                 float* f_px_out, dp_stream_t stream) {
+  if (!canonical || !depth || (!use_given && !fov_deg)) return DP_ERR_ARG;
+  if (H <= 0 || W <= 0 || SH <= 0 || SW <= 0) return DP_ERR_SHAPE;
+  // reference: inverse_depth = canonical * (W / f_px) with W / f_px a Python (double) scalar
+  const float given_scale = use_given ? (float)((double)W / f_given) : 0.f;
+  hipLaunchKernelGGL(infer_epi_kernel, dim3(blocks_for((long long)H * W, 256)), dim3(256), 0, (hipStream_t)stream,
+                     canonical, SH, SW, fov_deg, use_given, given_scale, (float)f_given, H, W, depth, f_px_out);
+  DP_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,253 @@
+"""Drop-in `depth_pro` model API backed by the MI355X engine.
+
+Mirrors the reference module `src/depth_pro/depth_pro.py`:
+  DepthProConfig / DEFAULT_MONODEPTH_CONFIG_DICT   (:26-46)
+  create_model_and_transforms(config, device, precision) -> (DepthPro, transform)   (:72-151)
+  DepthPro.img_size (:213-216), DepthPro.forward (:218-241), DepthPro.infer (:243-298)
+
+Same names, argument meanings, state-dict keys (1,119, strict loading) and
+error behaviour (KeyError for an unknown preset or bad checkpoint keys,
+AssertionError for a non-1536^2 `forward` input).  Differences, by design:
+  * the arithmetic runs in libdp_mi355x.so HIP kernels on a ROCm device (bf16
+    by default, f16 for precision=torch.half); a CPU device or a missing
+    library raises instead of computing anything on the host;
+  * with `checkpoint_uri=None` the weights are the deterministic synthetic set
+    of `depth_pro.weights` (the reference leaves PyTorch's random init).
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Mapping, Optional, Tuple, Union
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import ops
+from ._lib import DP_BF16, DP_F16, DPError, load
+from .engine import Engine, pack_weights
+from .spec import IMG_SIZE, param_spec
+from .weights import synthetic_state_dict
+
+ViTPreset = str
+VIT_PRESETS = ("dinov2l16_384",)
+
+
+@dataclass
+class DepthProConfig:
+    """Configuration for DepthPro (reference depth_pro.py:26-37)."""
+
+    patch_encoder_preset: ViTPreset
+    image_encoder_preset: ViTPreset
+    decoder_features: int
+
+    checkpoint_uri: Optional[str] = None
+    fov_encoder_preset: Optional[ViTPreset] = None
+    use_fov_head: bool = True
+
+
+DEFAULT_MONODEPTH_CONFIG_DICT = DepthProConfig(
+    patch_encoder_preset="dinov2l16_384",
+    image_encoder_preset="dinov2l16_384",
+    checkpoint_uri="./checkpoints/depth_pro.pt",
+    decoder_features=256,
+    use_fov_head=True,
+    fov_encoder_preset="dinov2l16_384",
+)
+
+
+def _check_preset(preset: ViTPreset) -> None:
+    if preset not in VIT_PRESETS:
+        raise KeyError(f"Preset {preset} not found.")  # depth_pro.py:67
+
+
+def _compute_dtype(precision: torch.dtype) -> int:
+    env = os.environ.get("DEPTH_PRO_COMPUTE_DTYPE", "").lower()
+    if env in ("fp16", "f16", "half", "float16"):
+        return DP_F16
+    if env in ("bf16", "bfloat16"):
+        return DP_BF16
+    return DP_F16 if precision == torch.half else DP_BF16
+
+
+class Transform:
+    """transform(image) for uint8 HxWx3 input (reference Compose, depth_pro.py:125-132).
+
+    The uint8 frame is uploaded as-is (7 MB at 1536^2 instead of 28 MB fp32) and
+    normalised to (x/255 - 0.5)/0.5 on the GPU by `dp_normalize_u8`.
+    """
+
+    def __init__(self, device: torch.device, precision: torch.dtype):
+        self.device = device
+        self.precision = precision
+
+    def __call__(self, image) -> torch.Tensor:
+        a = np.asarray(image)
+        if a.ndim == 2:
+            a = a[:, :, None]
+        if a.dtype != np.uint8 or a.shape[2] != 3:
+            raise TypeError(f"transform expects an HxWx3 uint8 image, got {a.dtype} {a.shape}")
+        src = torch.from_numpy(np.ascontiguousarray(a)).to(self.device, non_blocking=True)
+        out = torch.empty(3, a.shape[0], a.shape[1], dtype=self.precision, device=self.device)
+        ops.normalize_u8(src, out)
+        return out
+
+
+def _module_tree(spec, device, dtype) -> nn.Module:
+    root = nn.Module()
+    for name, shape in spec.items():
+        *path, leaf = name.split(".")
+        mod = root
+        for p in path:
+            if p not in mod._modules:
+                mod.add_module(p, nn.Module())
+            mod = mod._modules[p]
+        mod.register_parameter(leaf, nn.Parameter(torch.empty(shape, device=device, dtype=dtype),
+                                                  requires_grad=False))
+    return root
+
+
+class DepthPro(nn.Module):
+    """DepthPro network (reference depth_pro.py:154-298) on the MI355X engine."""
+
+    def __init__(self, use_fov_head: bool = True, device=torch.device("cpu"), compute_dtype: int = DP_BF16):
+        super().__init__()
+        tree = _module_tree(param_spec(use_fov_head), device, torch.float32)
+        for name, child in tree.named_children():
+            self.add_module(name, child)
+        self.use_fov_head = use_fov_head
+        self.compute_dtype = compute_dtype
+        self._engine: Optional[Engine] = None
+        self._use_graph = os.environ.get("DEPTH_PRO_HIPGRAPH", "0") == "1"
+
+    # -- engine lifecycle
+    def _invalidate(self):
+        self._engine = None
+
+    def _apply(self, fn, *a, **k):
+        self._invalidate()
+        return super()._apply(fn, *a, **k)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        self._invalidate()
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def engine(self) -> Engine:
+        if self._engine is None:
+            dev = next(self.parameters()).device
+            if dev.type != "cuda":
+                raise DPError("DepthPro (MI355X engine) runs on a ROCm device; got device "
+                              f"{dev} -- there is no CPU path")
+            load()
+            with torch.no_grad():
+                packed = pack_weights(dict(self.state_dict()), dev, self.compute_dtype)
+            self._engine = Engine(packed, dev, self.compute_dtype, use_fov=self.use_fov_head)
+            if self._use_graph:
+                self._engine.capture_graph()
+        return self._engine
+
+    def use_hip_graph(self, enable: bool = True) -> "DepthPro":
+        """Replay the whole forward as one captured HIP graph (static shapes)."""
+        self._use_graph = enable
+        if self._engine is not None:
+            if enable and self._engine.graph is None:
+                self._engine.capture_graph()
+            if not enable:
+                self._engine.graph = None
+        return self
+
+    @property
+    def img_size(self) -> int:
+        """Return the internal image size of the network (1536)."""
+        return IMG_SIZE
+
+    def _run_frame(self, x3: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """x3: (3, S, S) network-resolution frame on device -> engine outputs (static buffers)."""
+        eng = self.engine()
+        ops.resize_bilinear(x3, eng.x0)  # dtype conversion / copy into the static input
+        return eng.run()
+
+    def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """Canonical inverse depth (B,1,1536,1536) and FOV in degrees (B,1,1,1)."""
+        _, _, H, W = x.shape
+        assert H == self.img_size and W == self.img_size
+        outs, fovs = [], []
+        for b in range(x.shape[0]):
+            canonical, fov = self._run_frame(x[b])
+            outs.append(canonical.clone())
+            fovs.append(fov.clone())
+        canonical = torch.cat(outs, 0)
+        fov_deg = torch.cat(fovs, 0) if self.use_fov_head else None
+        return canonical, fov_deg
+
+    @torch.no_grad()
+    def infer(
+        self,
+        x: torch.Tensor,
+        f_px: Optional[Union[float, torch.Tensor]] = None,
+        interpolation_mode="bilinear",
+    ) -> Mapping[str, torch.Tensor]:
+        """Infer depth [m] and focal length [px] (reference depth_pro.py:243-298)."""
+        if interpolation_mode != "bilinear":
+            raise NotImplementedError("only interpolation_mode='bilinear' (the reference default) is supported")
+        if len(x.shape) == 3:
+            x = x.unsqueeze(0)
+        _, _, H, W = x.shape
+        eng = self.engine()
+        # prologue: (resize to) 1536^2 fp32 straight into the engine's static input
+        ops.resize_bilinear(x[0], eng.x0)
+        canonical, fov_deg = eng.run()
+        depth = torch.empty(H, W, dtype=torch.float32, device=x.device)
+        if f_px is None:
+            if not self.use_fov_head:
+                raise TypeError("f_px is required when the model has no FOV head")
+            f_out = torch.empty((), dtype=torch.float32, device=x.device)
+            ops.infer_epilogue(canonical, fov_deg, None, H, W, depth, f_out)
+            f_px = f_out
+        else:
+            given = float(f_px.detach().float().reshape(-1)[0].item()) if torch.is_tensor(f_px) else float(f_px)
+            ops.infer_epilogue(canonical, None, given, H, W, depth, None)
+            f_px = f_px.squeeze()  # mirrors depth_pro.py:286 (a plain Python float has no .squeeze)
+        return {"depth": depth.squeeze(), "focallength_px": f_px}
+
+
+def create_model_and_transforms(
+    config: DepthProConfig = DEFAULT_MONODEPTH_CONFIG_DICT,
+    device: torch.device = torch.device("cpu"),
+    precision: torch.dtype = torch.float32,
+    seed: int = 0,
+) -> Tuple[DepthPro, Transform]:
+    """Create a DepthPro model and load weights from `config.checkpoint_uri`.
+
+    Reference: depth_pro.py:72-151.  `seed` picks the synthetic weight set used
+    when `config.checkpoint_uri` is None.
+    """
+    _check_preset(config.patch_encoder_preset)
+    _check_preset(config.image_encoder_preset)
+    use_fov = bool(config.use_fov_head and config.fov_encoder_preset is not None)
+    if use_fov:
+        _check_preset(config.fov_encoder_preset)
+    if config.decoder_features != 256:
+        raise KeyError(f"decoder_features={config.decoder_features} not supported (the dinov2l16_384 model uses 256)")
+    device = torch.device(device)
+    model = DepthPro(use_fov_head=use_fov, device=torch.device("cpu"), compute_dtype=_compute_dtype(precision))
+
+    if config.checkpoint_uri is not None:
+        state_dict = torch.load(config.checkpoint_uri, map_location="cpu", weights_only=True)
+    else:
+        state_dict = synthetic_state_dict(seed, use_fov_head=use_fov)
+    missing_keys, unexpected_keys = model.load_state_dict(state_dict=state_dict, strict=True)
+    if len(unexpected_keys) != 0:
+        raise KeyError(f"Found unexpected keys when loading monodepth: {unexpected_keys}")
+    missing_keys = [key for key in missing_keys if "fc_norm" not in key]
+    if len(missing_keys) != 0:
+        raise KeyError(f"Keys are missing when loading monodepth: {missing_keys}")
+    del state_dict
+    model = model.to(device)
+    if precision == torch.half:
+        model.half()
+    model.eval()
+    transform = Transform(device, precision)
+    return model, transform

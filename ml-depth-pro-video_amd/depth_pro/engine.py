@@ -1,0 +1,344 @@
+"""The MI355X forward engine: packed weights + static HBM workspace + HIP kernels.
+
+`Engine.forward(x0)` runs `DepthPro.forward` (reference `depth_pro.py:218-241`)
+for one 1536x1536 frame entirely through libdp_mi355x.so kernels on the
+current stream:
+
+  patchify (pyramid + 35 windows, encoder.py:151-263)
+  -> 3 x ViT-L/16 (patch x35 windows, image x1, fov x1; timm Block x24 each)
+  -> merge + project/upsample (encoder.py:190-324)
+  -> MultiresConvDecoder (decoder.py:74-206) -> head (depth_pro.py:182-207)
+  -> FOV head (fov.py:56-82)
+
+All buffers are allocated once per engine, so a forward is hipGraph-capturable
+(`capture_graph`).  Activations are token-major / NHWC in 16-bit (bf16 or
+f16), the ViT residual streams fp32.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import ops
+from ._lib import DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DPError, load
+from .spec import DEPTH, EMBED_DIM, HEADS, IMG_SIZE, MLP_DIM, TOKENS
+
+NWIN = 35
+TOK = TOKENS            # 577
+PTOK = TOKENS - 1       # 576
+D = EMBED_DIM
+
+
+# --------------------------------------------------------------------- packing
+def _conv_w(w: torch.Tensor, dt) -> torch.Tensor:
+    """Conv2d [Cout, Cin, kh, kw] -> B[Cout][(ky, kx, ci)]."""
+    co = w.shape[0]
+    return w.permute(0, 2, 3, 1).reshape(co, -1).to(dt).contiguous()
+
+
+def _deconv_w(w: torch.Tensor, dt) -> torch.Tensor:
+    """ConvTranspose2d [Cin, Cout, 2, 2] -> B[(dy, dx, co)][ci]."""
+    ci, co = w.shape[0], w.shape[1]
+    return w.permute(2, 3, 1, 0).reshape(4 * co, ci).to(dt).contiguous()
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().to(torch.float32).contiguous()
+
+
+def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: int) -> Dict[str, object]:
+    """Convert a (reference-named) state dict into GEMM-ready device tensors.
+
+    Linear weights stay [N][K]; conv weights become [Cout][ky][kx][Cin]; k2s2
+    deconvs [(dy,dx,Cout)][Cin].  Each decoder fusion's deconv (no bias) and the
+    1x1 out_conv that follows it (decoder.py:180-184) are linear with nothing in
+    between, so they are composed once here into one deconv with bias
+    (W'[ci,co] = sum_c Wd[ci,c] Wo[co,c]): the 1x1 pass at the upsampled
+    resolution disappears from the frame.
+    """
+    dt = ops.torch_dtype(dtype_code)
+    g = lambda k: sd[k].detach().to(device)  # noqa: E731
+    P: Dict[str, object] = {}
+    for vit in ("encoder.patch_encoder.", "encoder.image_encoder.", "fov.encoder.0."):
+        if vit + "cls_token" not in sd:
+            continue
+        P[vit + "cls"] = _f32(g(vit + "cls_token")).reshape(D)
+        P[vit + "pos"] = _f32(g(vit + "pos_embed")).reshape(TOK, D)
+        P[vit + "pe.w"] = g(vit + "patch_embed.proj.weight").reshape(D, -1).to(dt).contiguous()
+        P[vit + "pe.b"] = _f32(g(vit + "patch_embed.proj.bias"))
+        for i in range(DEPTH):
+            b = f"{vit}blocks.{i}."
+            for n in ("norm1.weight", "norm1.bias", "norm2.weight", "norm2.bias", "attn.qkv.bias",
+                      "attn.proj.bias", "mlp.fc1.bias", "mlp.fc2.bias", "ls1.gamma", "ls2.gamma"):
+                P[b + n] = _f32(g(b + n))
+            for n in ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight"):
+                P[b + n] = g(b + n).to(dt).contiguous()
+        P[vit + "norm.weight"] = _f32(g(vit + "norm.weight"))
+        P[vit + "norm.bias"] = _f32(g(vit + "norm.bias"))
+    # encoder project / upsample
+    for name, n_up in (("upsample_latent0", 3), ("upsample_latent1", 2), ("upsample0", 1),
+                       ("upsample1", 1), ("upsample2", 1)):
+        p = f"encoder.{name}."
+        P[p + "0"] = _conv_w(g(p + "0.weight"), dt)
+        for i in range(1, n_up + 1):
+            P[p + str(i)] = _deconv_w(g(p + f"{i}.weight"), dt)
+    P["encoder.upsample_lowres.w"] = _deconv_w(g("encoder.upsample_lowres.weight"), dt)
+    P["encoder.upsample_lowres.b"] = _f32(g("encoder.upsample_lowres.bias")).repeat(4)
+    P["encoder.fuse_lowres.w"] = _conv_w(g("encoder.fuse_lowres.weight"), dt)
+    P["encoder.fuse_lowres.b"] = _f32(g("encoder.fuse_lowres.bias"))
+    # decoder
+    for i in range(1, 5):
+        P[f"decoder.convs.{i}"] = _conv_w(g(f"decoder.convs.{i}.weight"), dt)
+    for i in range(5):
+        p = f"decoder.fusions.{i}."
+        for r in ("resnet1", "resnet2"):
+            for j in (1, 3):
+                P[p + f"{r}.{j}.w"] = _conv_w(g(p + f"{r}.residual.{j}.weight"), dt)
+                P[p + f"{r}.{j}.b"] = _f32(g(p + f"{r}.residual.{j}.bias"))
+        wo = _f32(g(p + "out_conv.weight"))[:, :, 0, 0]  # [co, c]
+        bo = _f32(g(p + "out_conv.bias"))
+        if i != 0:
+            wd = _f32(g(p + "deconv.weight"))  # [ci, c, 2, 2]
+            wc = torch.einsum("icyx,oc->ioyx", wd, wo)  # composed deconv [ci, co, 2, 2]
+            P[p + "up.w"] = _deconv_w(wc, dt)
+            P[p + "up.b"] = bo.repeat(4)
+        else:
+            P[p + "out.w"] = wo.to(dt).contiguous()
+            P[p + "out.b"] = bo
+    # head
+    P["head.0.w"] = _conv_w(g("head.0.weight"), dt)
+    P["head.0.b"] = _f32(g("head.0.bias"))
+    P["head.1.w"] = _deconv_w(g("head.1.weight"), dt)
+    P["head.1.b"] = _f32(g("head.1.bias")).repeat(4)
+    P["head.2.w"] = _conv_w(g("head.2.weight"), dt)
+    P["head.2.b"] = _f32(g("head.2.bias"))
+    P["head.4.w"] = _f32(g("head.4.weight")).reshape(-1)
+    P["head.4.b"] = float(sd["head.4.bias"].detach().float().reshape(-1)[0])
+    if "fov.encoder.1.weight" in sd:
+        P["fov.lin.w"] = g("fov.encoder.1.weight").to(dt).contiguous()
+        P["fov.lin.b"] = _f32(g("fov.encoder.1.bias"))
+        P["fov.down.w"] = _conv_w(g("fov.downsample.0.weight"), dt)
+        P["fov.down.b"] = _f32(g("fov.downsample.0.bias"))
+        P["fov.h0.w"] = _conv_w(g("fov.head.0.weight"), dt)
+        P["fov.h0.b"] = _f32(g("fov.head.0.bias"))
+        P["fov.h2.w"] = _conv_w(g("fov.head.2.weight"), dt)
+        P["fov.h2.b"] = _f32(g("fov.head.2.bias"))
+        P["fov.h4.w"] = _f32(g("fov.head.4.weight")).reshape(-1)
+        P["fov.h4.b"] = float(sd["fov.head.4.bias"].detach().float().reshape(-1)[0])
+    return P
+
+
+# ---------------------------------------------------------------------- engine
+class _ViTBuffers:
+    def __init__(self, rows: int, dt, dev):
+        self.rows = rows
+        self.x = torch.empty(rows, D, dtype=torch.float32, device=dev)
+        self.h = torch.empty(rows, D, dtype=dt, device=dev)
+        self.qkv = torch.empty(rows, 3 * D, dtype=dt, device=dev)
+        self.a = torch.empty(rows, D, dtype=dt, device=dev)
+        self.m = torch.empty(rows, MLP_DIM, dtype=dt, device=dev)
+
+
+class Engine:
+    """One frame (batch 1) per forward; static workspace (~4 GB)."""
+
+    def __init__(self, packed: Dict[str, object], device: torch.device, dtype_code: int,
+                 use_fov: bool = True):
+        load()
+        if device.type != "cuda":
+            raise DPError("the MI355X Depth Pro engine needs a ROCm/HIP device")
+        if dtype_code not in (DP_BF16, DP_F16):
+            raise DPError("compute dtype must be bf16 or f16")
+        self.P = packed
+        self.dev = device
+        self.code = dtype_code
+        self.dt = ops.torch_dtype(dtype_code)
+        self.use_fov = use_fov and "fov.lin.w" in packed
+        dt, dev = self.dt, device
+        e = lambda *s, dtype=None: torch.empty(*s, dtype=dtype or dt, device=dev)  # noqa: E731
+        S = IMG_SIZE
+        self.x0 = e(3, S, S, dtype=torch.float32)           # network input (normalized, 1536^2)
+        self.cols = e(NWIN * PTOK, 768)
+        self.vp = _ViTBuffers(NWIN * TOK, dt, dev)          # patch encoder (35 windows)
+        self.vi = _ViTBuffers(TOK, dt, dev)                 # image encoder
+        self.vf = _ViTBuffers(TOK, dt, dev) if self.use_fov else None
+        # merged encoder maps (NHWC)
+        self.lat0 = e(96 * 96, D)
+        self.lat1 = e(96 * 96, D)
+        self.f0 = e(96 * 96, D)
+        self.f1 = e(48 * 48, D)
+        self.f2 = e(24 * 24, D)
+        self.g = e(24 * 24, D)
+        # upsample chains
+        self.t96_256 = e(96 * 96, 256)
+        self.t192_256 = e(192 * 192, 256)
+        self.t384_256 = e(384 * 384, 256)
+        self.enc0 = e(768 * 768, 256)
+        self.t96_256b = e(96 * 96, 256)
+        self.t192_256b = e(192 * 192, 256)
+        self.enc1 = e(384 * 384, 256)
+        self.t96_512 = e(96 * 96, 512)
+        self.enc2 = e(192 * 192, 512)
+        self.t48_1024 = e(48 * 48, D)
+        self.enc3 = e(96 * 96, D)
+        self.t24_1024 = e(24 * 24, D)
+        self.cat = e(48 * 48, 2 * D)
+        self.enc4 = e(48 * 48, D)
+        # decoder (one set of scratch maps per resolution)
+        self.dec = {}
+        for s in (48, 96, 192, 384, 768):
+            self.dec[s] = {k: e(s * s, 256) for k in ("c", "t", "x", "y")}
+        self.low = self.dec[48]["c"]
+        self.up = {s: e(s * s, 256) for s in (96, 192, 384, 768)}
+        self.feats = e(768 * 768, 256)
+        # head
+        self.h0 = e(768 * 768, 128)
+        self.h1 = e(1536 * 1536, 128)
+        self.canonical = e(1, 1, S, S, dtype=torch.float32)
+        # fov
+        self.fov_tok = e(PTOK, 128)
+        self.fx = e(24 * 24, 128)
+        self.f12 = e(12 * 12, 64)
+        self.f6 = e(6 * 6, 32)
+        self.fov_deg = e(1, 1, 1, 1, dtype=torch.float32)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+    # ------------------------------------------------------------------ ViT
+    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
+        P, M = self.P, n_img * TOK
+        # patch embed (k16 s16 conv as GEMM over the im2col rows) + bias + pos -> rows 1..576
+        ops.gemm(self.cols, P[pre + "pe.w"], buf.x, M=n_img * PTOK, N=D, K=768,
+                 A_off=cols_off_rows * 768, bias=P[pre + "pe.b"], pos=P[pre + "pos"], ldpos=D,
+                 pos_group=PTOK, pos_off=1, row_group=PTOK, row_group_out=TOK, row_off=1)
+        ops.vit_cls_rows(buf.x, P[pre + "cls"], P[pre + "pos"], n_img)
+        for i in range(DEPTH):
+            b = f"{pre}blocks.{i}."
+            ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
+            ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"])
+            ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS)
+            ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
+                     gamma=P[b + "ls1.gamma"], accumulate=True)
+            ops.layernorm(buf.x, P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, M, D)
+            ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
+                     act=DP_ACT_GELU)
+            ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
+                     gamma=P[b + "ls2.gamma"], accumulate=True)
+            if hooks and i in hooks:
+                hooks[i]()
+        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.h, M, D)
+
+    # -------------------------------------------------------- conv helpers
+    def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
+               stride=1, head_w=None, head_b=0.0):
+        s_out = (s_in + 2 - 3) // stride + 1
+        ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
+                 conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
+                 relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout,
+                 head_w=head_w, head_b=head_b, ldc=cout)
+
+    def _deconv(self, x, s_in, cin, w, out, cout, bias=None, C_off=0, ldc=None):
+        ops.gemm(x, w, out, M=s_in * s_in, N=4 * cout, K=cin, bias=bias, deconv=(s_in, s_in, cout),
+                 C_off=C_off, ldc=cout if ldc is None else ldc)
+
+    def _resblock(self, pre: str, x, s, out, extra=None):
+        """out = x (+ extra) + conv(relu(conv(relu(x)))) at s x s x 256."""
+        t = self.dec[s]["t"]
+        P = self.P
+        self._conv3(x, s, 256, P[pre + ".1.w"], t, 256, bias=P[pre + ".1.b"], relu_a=True, act=DP_ACT_RELU)
+        self._conv3(t, s, 256, P[pre + ".3.w"], out, 256, bias=P[pre + ".3.b"], R1=x, R2=extra)
+
+    def _fusion(self, i: int, feats, s, x1):
+        """FeatureFusionBlock2d i at resolution s (output at 2s for i != 0)."""
+        P, d = self.P, self.dec[s]
+        p = f"decoder.fusions.{i}."
+        x = feats
+        if x1 is not None:
+            self._resblock(p + "resnet1", x1, s, d["x"], extra=feats)
+            x = d["x"]
+        self._resblock(p + "resnet2", x, s, d["y"])
+        if i != 0:
+            out = self.up[2 * s]
+            self._deconv(d["y"], s, 256, P[p + "up.w"], out, 256, bias=P[p + "up.b"])
+            return out
+        ops.gemm(d["y"], P[p + "out.w"], self.feats, M=s * s, N=256, K=256, bias=P[p + "out.b"])
+        return self.feats
+
+    # -------------------------------------------------------------- forward
+    def forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Run the network on `self.x0`; results in self.canonical / self.fov_deg."""
+        P = self.P
+        ops.patchify_pyramid(self.x0, self.cols)
+        vp = self.vp
+        hooks = {
+            5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
+            11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
+        }
+        self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks)
+        ops.merge_windows(vp.h, 0, 5, 3, self.f0)
+        ops.merge_windows(vp.h, 25, 3, 6, self.f1)
+        ops.merge_windows(vp.h, 34, 1, 0, self.f2)
+        self._vit("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
+        ops.merge_windows(self.vi.h, 0, 1, 0, self.g)
+        # project / upsample (encoder.py:314-324)
+        e = "encoder."
+        ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
+        self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
+        self._deconv(self.t192_256, 192, 256, P[e + "upsample_latent0.2"], self.t384_256, 256)
+        self._deconv(self.t384_256, 384, 256, P[e + "upsample_latent0.3"], self.enc0, 256)
+        ops.gemm(self.lat1, P[e + "upsample_latent1.0"], self.t96_256b, M=96 * 96, N=256, K=D)
+        self._deconv(self.t96_256b, 96, 256, P[e + "upsample_latent1.1"], self.t192_256b, 256)
+        self._deconv(self.t192_256b, 192, 256, P[e + "upsample_latent1.2"], self.enc1, 256)
+        ops.gemm(self.f0, P[e + "upsample0.0"], self.t96_512, M=96 * 96, N=512, K=D)
+        self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
+        ops.gemm(self.f1, P[e + "upsample1.0"], self.t48_1024, M=48 * 48, N=D, K=D)
+        self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
+        ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
+        self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
+        self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
+                     C_off=D, ldc=2 * D)
+        ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
+        # decoder (decoder.py:74-93)
+        self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)
+        f = self._fusion(4, self.low, 48, None)
+        for i, (enc, s, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)), (1, (self.enc1, 384, 256))):
+            c = self.dec[s]["c"]
+            self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
+            f = self._fusion(i, f, s, c)
+        feats = self._fusion(0, f, 768, self.enc0)
+        # head (depth_pro.py:182-207): conv3x3 -> deconv -> conv3x3+ReLU -> 1x1+ReLU (fused)
+        self._conv3(feats, 768, 256, P["head.0.w"], self.h0, 128, bias=P["head.0.b"])
+        self._deconv(self.h0, 768, 128, P["head.1.w"], self.h1, 128, bias=P["head.1.b"])
+        self._conv3(self.h1, 1536, 128, P["head.2.w"], self.canonical, 32, bias=P["head.2.b"], act=DP_ACT_RELU,
+                    head_w=P["head.4.w"], head_b=P["head.4.b"])
+        # FOV (fov.py:56-82)
+        if self.use_fov:
+            vf = self.vf
+            self._vit("fov.encoder.0.", vf, 1, 34 * PTOK)
+            ops.gemm(vf.h, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
+            self._conv3(self.low, 48, 256, P["fov.down.w"], self.fx, 128, bias=P["fov.down.b"], act=DP_ACT_RELU,
+                        R1=self.fov_tok, stride=2)
+            self._conv3(self.fx, 24, 128, P["fov.h0.w"], self.f12, 64, bias=P["fov.h0.b"], act=DP_ACT_RELU, stride=2)
+            self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
+            ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
+        return self.canonical, self.fov_deg
+
+    # ---------------------------------------------------------------- graphs
+    def capture_graph(self) -> None:
+        """Capture `forward` into a HIP graph (static shapes); replay with `run`."""
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            self.forward()  # warm-up outside capture (first-launch code object loads)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.forward()
+        self.graph = g
+
+    def run(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.graph is not None:
+            self.graph.replay()
+            return self.canonical, self.fov_deg
+        return self.forward()

@@ -1,0 +1,186 @@
+"""Typed launchers: torch tensors -> C-ABI calls on the current HIP stream.
+
+Every function takes device tensors (PyTorch owns the memory), passes their
+`data_ptr()` and the current stream to libdp_mi355x.so and raises
+`_lib.DPError` on any non-zero return.  Nothing here computes on the host.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import (DP_A_CONV, DP_A_DENSE, DP_ACT_NONE, DP_BF16, DP_F16, DP_F32,
+                   DP_STORE_DECONV2X2, DP_STORE_ROWS, GemmArgs, check)
+
+_TORCH_DT = {DP_BF16: torch.bfloat16, DP_F16: torch.float16, DP_F32: torch.float32}
+
+
+def torch_dtype(code: int) -> torch.dtype:
+    return _TORCH_DT[code]
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    for k, v in _TORCH_DT.items():
+        if v == dt:
+            return k
+    raise _lib.DPError(f"unsupported dtype {dt}")
+
+
+# Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, ev0, ev1).
+_PROF: Optional[list] = None
+
+
+def profile_begin() -> None:
+    global _PROF
+    _PROF = []
+
+
+def profile_end() -> list:
+    """Stop recording; returns [(kind, flops, milliseconds)] (synchronizes)."""
+    global _PROF
+    rec, _PROF = _PROF or [], None
+    torch.cuda.synchronize()
+    return [(k, f, a.elapsed_time(b)) for (k, f, a, b) in rec]
+
+
+class _Timed:
+    def __init__(self, kind: str, flops: float):
+        self.kind, self.flops = kind, flops
+
+    def __enter__(self):
+        if _PROF is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _PROF is not None:
+            self.e1.record()
+            _PROF.append((self.kind, self.flops, self.e0, self.e1))
+        return False
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K: int,
+         lda: Optional[int] = None, ldb: Optional[int] = None, ldc: Optional[int] = None,
+         conv: Optional[dict] = None, relu_a: bool = False,
+         bias: Optional[torch.Tensor] = None, act: int = DP_ACT_NONE,
+         gamma: Optional[torch.Tensor] = None,
+         pos: Optional[torch.Tensor] = None, ldpos: int = 0, pos_group: int = 0, pos_off: int = 0,
+         R1: Optional[torch.Tensor] = None, ldr1: int = 0,
+         R2: Optional[torch.Tensor] = None, ldr2: int = 0,
+         accumulate: bool = False, deconv: Optional[tuple] = None,
+         row_group: int = 0, row_group_out: int = 0, row_off: int = 0,
+         head_w: Optional[torch.Tensor] = None, head_b: float = 0.0,
+         A_off: int = 0, C_off: int = 0, tile: int = 0) -> None:
+    """dp_gemm. `A_off`/`C_off` are element offsets into A / C (sub-views)."""
+    a = GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.dtype = dtype_code(B.dtype)
+    a.A = A.data_ptr() + A_off * A.element_size()
+    a.lda = K if lda is None else lda
+    a.B = B.data_ptr()
+    a.ldb = K if ldb is None else ldb
+    if conv is not None:
+        a.a_mode = DP_A_CONV
+        a.in_h, a.in_w, a.in_c = conv["in_h"], conv["in_w"], conv["in_c"]
+        a.k_h, a.k_w = conv["k"], conv["k"]
+        a.stride, a.pad = conv.get("stride", 1), conv.get("pad", 0)
+        a.out_h, a.out_w = conv["out_h"], conv["out_w"]
+        a.lda = 0
+    else:
+        a.a_mode = DP_A_DENSE
+    a.relu_a = int(relu_a)
+    a.bias = _p(bias)
+    a.act = act
+    a.gamma = _p(gamma)
+    a.pos = _p(pos)
+    a.ldpos, a.pos_group, a.pos_off = ldpos, pos_group, pos_off
+    a.R1, a.ldr1 = _p(R1), ldr1
+    a.R2, a.ldr2 = _p(R2), ldr2
+    a.C = C.data_ptr() + C_off * C.element_size()
+    a.ldc = N if ldc is None else ldc
+    a.c_dtype = dtype_code(C.dtype)
+    a.accumulate = int(accumulate)
+    if deconv is not None:
+        a.store_mode = DP_STORE_DECONV2X2
+        a.dc_h, a.dc_w, a.dc_cout = deconv
+    else:
+        a.store_mode = DP_STORE_ROWS
+    a.row_group, a.row_group_out, a.row_off = row_group, row_group_out, row_off
+    a.head_w = _p(head_w)
+    a.head_b = float(head_b)
+    a.tile = tile
+    kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
+    with _Timed(kind, 2.0 * M * N * K):
+        check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
+
+
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor, rows: int, cols: int,
+              eps: float = 1e-6) -> None:
+    with _Timed("layernorm", 0.0):
+        check(_lib.load().dp_layernorm(x.data_ptr(), cols, w.data_ptr(), b.data_ptr(), y.data_ptr(), cols,
+                                       rows, cols, eps, dtype_code(y.dtype), _stream(y)), "dp_layernorm")
+
+
+def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int = 16,
+              head_dim: int = 64) -> None:
+    with _Timed("attention", 4.0 * batch * heads * seq * seq * head_dim):
+        check(_lib.load().dp_attention(qkv.data_ptr(), out.data_ptr(), batch, seq, heads, head_dim,
+                                       head_dim ** -0.5, dtype_code(out.dtype), _stream(out)), "dp_attention")
+
+
+def normalize_u8(img: torch.Tensor, out: torch.Tensor) -> None:
+    H, W = img.shape[0], img.shape[1]
+    check(_lib.load().dp_normalize_u8(img.data_ptr(), H, W, out.data_ptr(), dtype_code(out.dtype),
+                                      _stream(out)), "dp_normalize_u8")
+
+
+def resize_bilinear(src: torch.Tensor, dst: torch.Tensor) -> None:
+    src = src.contiguous()
+    C, H, W = src.shape[-3:]
+    OH, OW = dst.shape[-2:]
+    check(_lib.load().dp_resize_bilinear(src.data_ptr(), dtype_code(src.dtype), C, H, W, dst.data_ptr(),
+                                         OH, OW, _stream(dst)), "dp_resize_bilinear")
+
+
+def patchify_pyramid(x0: torch.Tensor, cols: torch.Tensor) -> None:
+    check(_lib.load().dp_patchify_pyramid(x0.data_ptr(), cols.data_ptr(), dtype_code(cols.dtype),
+                                          _stream(cols)), "dp_patchify_pyramid")
+
+
+def vit_cls_rows(x: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor, n: int) -> None:
+    check(_lib.load().dp_vit_cls_rows(x.data_ptr(), cls.data_ptr(), pos.data_ptr(), n, _stream(x)),
+          "dp_vit_cls_rows")
+
+
+def merge_windows(src: torch.Tensor, first_window: int, steps: int, padding: int, dst: torch.Tensor,
+                  ld: int = 1024) -> None:
+    check(_lib.load().dp_merge_windows(src.data_ptr(), dtype_code(src.dtype), ld, first_window, steps, padding,
+                                       dst.data_ptr(), dtype_code(dst.dtype), _stream(dst)), "dp_merge_windows")
+
+
+def fov_tail(x6: torch.Tensor, w: torch.Tensor, bias: float, out: torch.Tensor) -> None:
+    check(_lib.load().dp_fov_tail(x6.data_ptr(), dtype_code(x6.dtype), w.data_ptr(), float(bias),
+                                  out.data_ptr(), _stream(out)), "dp_fov_tail")
+
+
+def infer_epilogue(canonical: torch.Tensor, fov_deg: Optional[torch.Tensor], f_given: Optional[float],
+                   H: int, W: int, depth: torch.Tensor, f_px_out: Optional[torch.Tensor]) -> None:
+    SH, SW = canonical.shape[-2:]
+    use_given = f_given is not None
+    check(_lib.load().dp_infer_epilogue(canonical.data_ptr(), SH, SW, _p(fov_deg), int(use_given),
+                                        float(f_given) if use_given else 0.0, H, W, depth.data_ptr(),
+                                        _p(f_px_out), _stream(depth)), "dp_infer_epilogue")

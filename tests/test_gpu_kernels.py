@@ -1,0 +1,229 @@
+"""Per-kernel parity of libdp_mi355x.so against plain PyTorch fp32 references.
+
+Tolerances: inputs are exactly representable in the 16-bit compute type, so the
+only error sources are fp32 accumulation order and the final rounding of a
+16-bit output (relative 2^-8 for bf16, 2^-11 for f16).
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from depth_pro import ops  # noqa: E402
+from depth_pro._lib import DP_ACT_GELU, DP_ACT_RELU  # noqa: E402
+
+DTYPES = [torch.bfloat16, torch.float16]
+
+
+def rnd(*shape, dt, dev, scale=1.0, gen=None):
+    return (torch.randn(*shape, generator=gen) * scale).to(dt).to(dev)
+
+
+def tol(dt):
+    return 2e-2 if dt == torch.bfloat16 else 4e-3
+
+
+def close(out, ref, dt, what):
+    out, ref = out.float().cpu(), ref.float().cpu()
+    err = (out - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= tol(dt) * scale, f"{what}: max|d|={err:.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,K", [(577, 3072, 1024), (1000, 128, 64), (257, 32, 128), (20195, 1024, 1024)])
+def test_gemm_dense_bias(cuda, dt, M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    C = torch.empty(M, N, dtype=dt, device=cuda)
+    ops.gemm(A, B, C, M=M, N=N, K=K, bias=bias)
+    ref = A.float() @ B.float().t() + bias
+    close(C, ref, dt, "gemm")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_gelu_and_residual_accumulate(cuda, dt):
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 700, 1024, 4096
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    gamma = torch.rand(N, generator=g).to(cuda)
+    X = torch.randn(M, N, generator=g).to(cuda)
+    C = X.clone()
+    ops.gemm(A, B, C, M=M, N=N, K=K, bias=bias, gamma=gamma, accumulate=True)
+    ref = X + gamma * (A.float() @ B.float().t() + bias)
+    close(C, ref, torch.float32 if dt == torch.float16 else dt, "proj+ls+residual")
+    H = torch.empty(M, N, dtype=dt, device=cuda)
+    ops.gemm(A, B, H, M=M, N=N, K=K, bias=bias, act=DP_ACT_GELU)
+    close(H, F.gelu(A.float() @ B.float().t() + bias), dt, "fc1+gelu")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_patch_embed_rows_pos(cuda, dt):
+    g = torch.Generator().manual_seed(5)
+    n, K, N = 3, 768, 1024
+    A = rnd(n * 576, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    pos = torch.randn(577, N, generator=g).to(cuda)
+    cls = torch.randn(N, generator=g).to(cuda)
+    X = torch.full((n * 577, N), float("nan"), device=cuda)
+    ops.gemm(A, B, X, M=n * 576, N=N, K=K, bias=bias, pos=pos, ldpos=N, pos_group=576, pos_off=1,
+             row_group=576, row_group_out=577, row_off=1)
+    ops.vit_cls_rows(X, cls, pos, n)
+    t = (A.float() @ B.float().t() + bias).reshape(n, 576, N)
+    ref = torch.cat((cls.expand(n, 1, N), t), 1) + pos
+    close(X.reshape(n, 577, N), ref, torch.float32, "patch-embed rows")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("S,cin,cout,stride", [(48, 1024, 256, 1), (96, 256, 256, 1), (48, 256, 128, 2),
+                                                (12, 64, 32, 2), (37, 128, 64, 1)])
+def test_conv3x3_implicit_gemm(cuda, dt, S, cin, cout, stride):
+    g = torch.Generator().manual_seed(S * cin + cout)
+    x = rnd(1, cin, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(cout, cin, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * cin) ** -0.5)
+    b = torch.randn(cout, generator=g).to(cuda)
+    r1 = rnd(1, cout, (S + 2 - 3) // stride + 1, (S + 2 - 3) // stride + 1, dt=dt, dev=cuda, gen=g)
+    so = (S + 2 - 3) // stride + 1
+    xh = x.permute(0, 2, 3, 1).contiguous()
+    wp = w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous()
+    r1h = r1.permute(0, 2, 3, 1).contiguous()
+    out = torch.empty(so * so, cout, dtype=dt, device=cuda)
+    ops.gemm(xh, wp, out, M=so * so, N=cout, K=9 * cin,
+             conv=dict(in_h=S, in_w=S, in_c=cin, k=3, stride=stride, pad=1, out_h=so, out_w=so),
+             relu_a=True, bias=b, act=DP_ACT_RELU, R1=r1h, ldr1=cout)
+    ref = F.relu(F.conv2d(F.relu(x.float()), w.float(), b, stride=stride, padding=1)) + r1.float()
+    close(out.reshape(1, so, so, cout).permute(0, 3, 1, 2), ref, dt, "conv3x3")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_deconv2x2_pixel_shuffle_store(cuda, dt):
+    g = torch.Generator().manual_seed(11)
+    S, cin, cout = 24, 1024, 512
+    x = rnd(1, cin, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(cin, cout, 2, 2, dt=dt, dev=cuda, gen=g, scale=cin ** -0.5)
+    b = torch.randn(cout, generator=g).to(cuda)
+    xh = x.permute(0, 2, 3, 1).reshape(S * S, cin).contiguous()
+    wp = w.permute(2, 3, 1, 0).reshape(4 * cout, cin).contiguous()
+    out = torch.zeros(2 * S * 2 * S, 2 * cout, dtype=dt, device=cuda)  # into a concat buffer, 2nd half
+    ops.gemm(xh, wp, out, M=S * S, N=4 * cout, K=cin, bias=b.repeat(4), deconv=(S, S, cout), C_off=cout, ldc=2 * cout)
+    ref = F.conv_transpose2d(x.float(), w.float(), b, stride=2)
+    got = out[:, cout:].reshape(1, 2 * S, 2 * S, cout).permute(0, 3, 1, 2)
+    close(got, ref, dt, "deconv")
+    assert out[:, :cout].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_head_conv_with_fused_1x1(cuda, dt):
+    g = torch.Generator().manual_seed(13)
+    S, cin = 40, 128
+    x = rnd(1, cin, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(32, cin, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * cin) ** -0.5)
+    b = torch.randn(32, generator=g).to(cuda)
+    w4 = torch.rand(32, generator=g).to(cuda)
+    out = torch.empty(S * S, dtype=torch.float32, device=cuda)
+    ops.gemm(x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).reshape(32, -1).contiguous(), out,
+             M=S * S, N=32, K=9 * cin, conv=dict(in_h=S, in_w=S, in_c=cin, k=3, stride=1, pad=1, out_h=S, out_w=S),
+             bias=b, act=DP_ACT_RELU, head_w=w4, head_b=0.25)
+    h = F.relu(F.conv2d(x.float(), w.float(), b, padding=1))
+    ref = F.relu(F.conv2d(h, w4.reshape(1, 32, 1, 1), torch.tensor([0.25], device=cuda)))
+    close(out.reshape(1, 1, S, S), ref, dt, "head conv+1x1")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("batch,seq", [(2, 577), (1, 100), (3, 64), (1, 1)])
+def test_attention(cuda, dt, batch, seq):
+    g = torch.Generator().manual_seed(seq)
+    H, hd = 16, 64
+    qkv = rnd(batch * seq, 3 * H * hd, dt=dt, dev=cuda, gen=g, scale=2.0)
+    out = torch.empty(batch * seq, H * hd, dtype=dt, device=cuda)
+    ops.attention(qkv, out, batch, seq, H, hd)
+    q, k, v = qkv.float().reshape(batch, seq, 3, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
+    ref = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(batch * seq, H * hd)
+    close(out, ref, dt, "attention")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_layernorm(cuda, dt):
+    g = torch.Generator().manual_seed(17)
+    x = (torch.randn(1234, 1024, generator=g) * 3 + 1).to(cuda)
+    w = torch.randn(1024, generator=g).to(cuda)
+    b = torch.randn(1024, generator=g).to(cuda)
+    y = torch.empty(1234, 1024, dtype=dt, device=cuda)
+    ops.layernorm(x, w, b, y, 1234, 1024)
+    close(y, F.layer_norm(x, (1024,), w, b, 1e-6), dt, "layernorm")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_patchify_pyramid_vs_oracle_split(cuda, dt):
+    from oracle import depth_pro_oracle as O
+
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(1, 3, 1536, 1536, generator=g)
+    cols = torch.empty(35 * 576, 768, dtype=dt, device=cuda)
+    ops.patchify_pyramid(x[0].to(cuda), cols)
+    x0, x1, x2 = O.pyramid(x)
+    wins = torch.cat((O.split(x0, 0.25), O.split(x1, 0.5), x2), 0)  # (35,3,384,384)
+    ref = F.unfold(wins, 16, stride=16).transpose(1, 2).reshape(35 * 576, 768)  # k = c*256+ky*16+kx
+    assert torch.equal(cols.cpu(), ref.to(dt)) or (cols.float().cpu() - ref).abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_merge_windows_vs_oracle(cuda, dt):
+    from oracle import depth_pro_oracle as O
+
+    g = torch.Generator().manual_seed(23)
+    tok = torch.randn(35 * 577, 1024, generator=g)
+    for (w0, steps, pad, S) in ((0, 5, 3, 96), (25, 3, 6, 48), (34, 1, 0, 24)):
+        dst = torch.empty(S * S, 1024, dtype=dt, device=cuda)
+        ops.merge_windows(tok.to(cuda), w0, steps, pad, dst)
+        win = O.tokens_to_nchw(tok.reshape(35, 577, 1024)[w0:w0 + steps * steps])
+        ref = O.merge(win, 1, pad)  # (1,1024,S,S)
+        assert torch.equal(dst.cpu(), ref[0].permute(1, 2, 0).reshape(S * S, 1024).to(dt))
+        dst2 = torch.empty_like(dst)
+        ops.merge_windows(tok.to(cuda).to(dt), w0, steps, pad, dst2)
+        assert torch.equal(dst2, dst)
+
+
+@pytest.mark.parametrize("HW", [(1536, 1536), (1080, 1920), (2268, 3024), (500, 333)])
+def test_resize_and_infer_epilogue(cuda, HW):
+    H, W = HW
+    g = torch.Generator().manual_seed(H)
+    x = torch.randn(3, H, W, generator=g)
+    out = torch.empty(3, 1536, 1536, device=cuda)
+    ops.resize_bilinear(x.to(cuda), out)
+    ref = F.interpolate(x[None], size=(1536, 1536), mode="bilinear", align_corners=False)[0]
+    assert (out.cpu() - ref).abs().max() < 1e-5
+    canon = torch.rand(1, 1, 1536, 1536, generator=g) * 3
+    fov = torch.tensor([[[[57.3]]]])
+    depth = torch.empty(H, W, device=cuda)
+    fpx = torch.empty((), device=cuda)
+    ops.infer_epilogue(canon.to(cuda), fov.to(cuda), None, H, W, depth, fpx)
+    f_ref = 0.5 * W / torch.tan(0.5 * torch.deg2rad(fov.float()))
+    inv = canon * (W / f_ref)
+    if (H, W) != (1536, 1536):
+        inv = F.interpolate(inv, size=(H, W), mode="bilinear", align_corners=False)
+    dref = 1.0 / torch.clamp(inv, 1e-4, 1e4)
+    assert abs(fpx.item() - f_ref.item()) <= 1e-5 * f_ref.item()
+    np.testing.assert_allclose(depth.cpu().numpy(), dref[0, 0].numpy(), rtol=2e-5, atol=1e-6)
+    ops.infer_epilogue(canon.to(cuda), None, 1234.5, H, W, depth, None)
+    inv = canon * (W / 1234.5)
+    if (H, W) != (1536, 1536):
+        inv = F.interpolate(inv, size=(H, W), mode="bilinear", align_corners=False)
+    np.testing.assert_allclose(depth.cpu().numpy(), (1.0 / torch.clamp(inv, 1e-4, 1e4))[0, 0].numpy(),
+                               rtol=2e-5, atol=1e-6)
+
+
+def test_normalize_u8(cuda):
+    img = np.random.default_rng(0).integers(0, 256, (300, 200, 3), dtype=np.uint8)
+    out = torch.empty(3, 300, 200, device=cuda)
+    ops.normalize_u8(torch.from_numpy(img).to(cuda), out)
+    ref = (torch.from_numpy(img).permute(2, 0, 1).float().div(255) - 0.5) / 0.5
+    assert torch.equal(out.cpu(), ref)
