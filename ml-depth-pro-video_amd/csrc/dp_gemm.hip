@@ -1,21 +1,30 @@
-// dp_gemm: LDS-tiled bf16/f16 MFMA GEMM with an implicit-conv A loader and a
-// fused epilogue, for gfx950 (CDNA4).
+// dp_gemm: bf16/f16 MFMA GEMM with an implicit-conv A loader and a fused
+// epilogue, for gfx950 (CDNA4).  Two tile engines share one epilogue:
 //
-// Tile: BM x BN x 64, 256 threads = 4 wave64s laid out WM x WN; each wave owns
-// a (BM/WM) x (BN/WN) sub-tile of 16x16 fragments computed with
-// v_mfma_f32_16x16x32_{bf16,f16}.  Operands are staged global -> VGPR -> LDS
-// (double-buffered, one barrier per K-tile); LDS rows are 128 B with the
-// chunk index XOR-swizzled by (row & 7) so the ds_read_b128 fragment reads are
-// bank-conflict free.  The MFMA is issued with the weight fragment as the
-// A-operand and the activation fragment as the B-operand, so D = C^T: every
-// lane ends up with 4 consecutive output channels of one output row, which
-// makes bias/gamma loads and the stores 8-16 B wide.
+// * "big" (256 x BN x 64, BN in {256, 128}; 512 threads = 8 wave64s as 2 x 4,
+//   each wave 128 x BN/4): operands stream global -> LDS directly with
+//   global_load_lds_dwordx4 (no VGPR staging) into a 2-stage LDS ring; the
+//   loads for K-tile t+2 are issued as soon as tile t has been consumed, so a
+//   whole tile of MFMA work covers their latency, and the waits are counted
+//   (`s_waitcnt vmcnt(N)` + raw `s_barrier`, never a full drain in the loop).
+//   1 workgroup per CU; the 256-row A panel halves L2->LDS traffic per FLOP
+//   compared with a 128^2 tile.  Block ids are remapped so that the blocks one
+//   XCD runs are a contiguous range of tiles (shared A panels stay in that
+//   XCD's L2).
+// * "small" (BM x BN x 64, 256 threads, register-staged, 2 workgroups/CU):
+//   N <= 64 outputs (depth-head tail, FOV head) and the fused 1x1 head.
+//
+// Both: LDS rows are 128 B (64 x 16-bit) with the 16-B chunk index XOR-swizzled
+// by (row & 7) -> conflict-free ds_read_b128 fragment reads.  The MFMA
+// v_mfma_f32_16x16x32_{bf16,f16} is issued with the weight fragment as its
+// A-operand and the activation fragment as B, so D = C^T: each lane ends up
+// with 4 consecutive output channels of one output row, and bias / gamma /
+// residual loads and the stores are 8-16 B per lane.
 #include "dp_common.h"
 
 namespace {
 
 constexpr int BK = 64;
-constexpr int NT = 256;
 
 struct GemmP {
   int M, N, K;
@@ -47,9 +56,272 @@ struct GemmP {
   int tiles_n;
 };
 
-__device__ __forceinline__ int lds_off(int row, int chunk) {
+// 16 zero bytes x 8: source of the implicit-conv zero padding for LDS-DMA loads
+__device__ __attribute__((aligned(16))) uint32_t g_zero_page[32];
+
+__device__ __forceinline__ int lds_off(int row, int chunk) {  // element offset, 64-wide rows
   return row * BK + ((chunk ^ (row & 7)) << 3);
 }
+
+// ---------------------------------------------------------------- epilogue
+// v[0..3] = accumulators of output (m, n..n+3).  Order: bias, act, gamma, pos,
+// R1, R2, (+C), store; with head_w the values are folded into hsum instead.
+template <typename K_>
+__device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float (&v)[4], float& hsum) {
+  if (p.bias) {
+    float4 b = *(const float4*)(p.bias + n);
+    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+  }
+  if (p.act == DP_ACT_RELU) {
+    #pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+  } else if (p.act == DP_ACT_GELU) {
+    #pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+  }
+  if (p.gamma) {
+    float4 g = *(const float4*)(p.gamma + n);
+    v[0] *= g.x; v[1] *= g.y; v[2] *= g.z; v[3] *= g.w;
+  }
+  if (p.pos) {
+    const float* pp = p.pos + (long long)(m % p.pos_group + p.pos_off) * p.ldpos + n;
+    float4 q = *(const float4*)pp;
+    v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+  }
+  if (p.R1) {
+    uint2 r = *(const uint2*)(p.R1 + (long long)m * p.ldr1 + n);
+    v[0] += K_::to_f(r.x & 0xffff); v[1] += K_::to_f(r.x >> 16);
+    v[2] += K_::to_f(r.y & 0xffff); v[3] += K_::to_f(r.y >> 16);
+  }
+  if (p.R2) {
+    uint2 r = *(const uint2*)(p.R2 + (long long)m * p.ldr2 + n);
+    v[0] += K_::to_f(r.x & 0xffff); v[1] += K_::to_f(r.x >> 16);
+    v[2] += K_::to_f(r.y & 0xffff); v[3] += K_::to_f(r.y >> 16);
+  }
+  if (p.head_w) {
+    float4 w = *(const float4*)(p.head_w + n);
+    hsum += v[0] * w.x + v[1] * w.y + v[2] * w.z + v[3] * w.w;
+    return;
+  }
+  long long off;
+  if (p.store_mode == DP_STORE_DECONV2X2) {
+    const int hw = p.dc_h * p.dc_w;
+    const int b = m / hw, rr = m - b * hw;
+    const int y = rr / p.dc_w, x = rr - y * p.dc_w;
+    const int q = n / p.dc_cout, co = n - q * p.dc_cout;
+    const long long pix = ((long long)b * 2 * p.dc_h + 2 * y + (q >> 1)) * (2 * p.dc_w) + 2 * x + (q & 1);
+    off = pix * p.ldc + co;
+  } else {
+    long long row = m;
+    if (p.row_group) row = (long long)(m / p.row_group) * p.row_group_out + p.row_off + m % p.row_group;
+    off = row * p.ldc + n;
+  }
+  if (p.c_dtype == DP_F32) {
+    float* c = (float*)p.C + off;
+    if (p.accumulate) {
+      float4 o = *(const float4*)c;
+      v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+    }
+    *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    uint2 o;
+    o.x = (uint32_t)K_::from_f(v[0]) | ((uint32_t)K_::from_f(v[1]) << 16);
+    o.y = (uint32_t)K_::from_f(v[2]) | ((uint32_t)K_::from_f(v[3]) << 16);
+    *(uint2*)((u16*)p.C + off) = o;
+  }
+}
+
+// implicit-conv row descriptor: output pixel m -> top-left input tap
+struct ConvRow {
+  int iy, ix, pix;
+};
+__device__ __forceinline__ ConvRow conv_row(const GemmP& p, int m) {
+  ConvRow r;
+  const bool ok = m < p.M;
+  const int mc = ok ? m : p.M - 1;
+  const int hw = p.out_h * p.out_w;
+  const int b = mc / hw, rr = mc - b * hw;
+  const int oy = rr / p.out_w, ox = rr - oy * p.out_w;
+  r.iy = ok ? oy * p.stride - p.pad : -(1 << 28);
+  r.ix = ox * p.stride - p.pad;
+  r.pix = b * p.in_h * p.in_w;
+  return r;
+}
+__device__ __forceinline__ const u16* conv_src(const GemmP& p, const ConvRow& r, int ky, int kx, int ci, bool& inb) {
+  const int iy = r.iy + ky, ix = r.ix + kx;
+  inb = (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+  const long long pix = (long long)r.pix + (long long)iy * p.in_w + ix;
+  return p.A + pix * p.in_c + ci;
+}
+
+// ============================================================ big-tile engine
+constexpr int NT_BIG = 512;
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// One 16-B-per-lane LDS-DMA piece (1 KiB per wave) written at the wave-uniform
+// LDS byte address `lds_dst`.  Issued from inline asm so the compiler does not
+// add its conservative `s_waitcnt vmcnt(0)` in front of every later ds_read:
+// completion is tracked by hand with the counted waits below.
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_dst)
+      : "memory");
+}
+
+template <typename K_, int BN, bool CONV, bool RELU>
+__global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
+  constexpr int BM = 256;
+  constexpr int WN = 4;
+  constexpr int TM = 128, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LA = BM * 8 / NT_BIG;  // 16-B LDS-DMA pieces per thread per A tile (4)
+  constexpr int LB = BN * 8 / NT_BIG;  // per B tile (4 or 2)
+  constexpr int LT = LA + LB;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // XCD-aware bijective remap (blocks b and b+8 share an XCD under round-robin dispatch)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  // LDS-DMA piece i of this thread: tile row i*64 + wave*8 + lane/8, LDS slot lane%8 holds
+  // logical chunk (lane%8) ^ (row&7) -> the swizzle is applied on the SOURCE address.
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  const u16* a_src[LA];
+  ConvRow a_cr[LA];
+  #pragma unroll
+  for (int i = 0; i < LA; ++i) {
+    const int m = m0 + i * 64 + prow;
+    if constexpr (CONV) {
+      a_cr[i] = conv_row(p, m);
+    } else {
+      a_src[i] = p.A + (long long)(m < p.M ? m : p.M - 1) * p.lda + pchunk * 8;
+    }
+  }
+  const u16* b_src[LB];
+  #pragma unroll
+  for (int i = 0; i < LB; ++i) {
+    const int n = n0 + i * 64 + prow;
+    b_src[i] = p.B + (long long)(n < p.N ? n : p.N - 1) * p.ldb + pchunk * 8;
+  }
+  int t_ky = 0, t_kx = 0, t_ci = 0;  // conv tap of the next K tile to issue (uniform)
+
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
+  auto issue = [&](int kt, int stage) {
+    const uint32_t sa = lds_base + stage * STAGE;
+    const uint32_t sb = sa + A_BYTES;
+    const int k0 = kt * BK;
+    #pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const void* src;
+      if constexpr (CONV) {
+        bool inb;
+        const u16* s = conv_src(p, a_cr[i], t_ky, t_kx, t_ci + pchunk * 8, inb);
+        src = inb ? (const void*)s : (const void*)g_zero_page;
+      } else {
+        src = a_src[i] + k0;
+      }
+      glds16(src, sa + i * 8192);
+    }
+    if constexpr (CONV) {
+      t_ci += BK;
+      if (t_ci == p.in_c) {
+        t_ci = 0;
+        if (++t_kx == p.k_w) { t_kx = 0; ++t_ky; }
+      }
+    }
+    #pragma unroll
+    for (int i = 0; i < LB; ++i) glds16(b_src[i] + k0, sb + i * 8192);
+  };
+
+  f32x4_t acc[FM][FN];
+  #pragma unroll
+  for (int i = 0; i < FM; ++i)
+    #pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fchunk = lane >> 4;
+  auto compute = [&](int stage) {
+    const u16* sa = (const u16*)(smem + stage * STAGE);
+    const u16* sb = (const u16*)(smem + stage * STAGE + A_BYTES);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 bf[FN];
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *(const uint4*)(sb + lds_off(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      #pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        uint4 af = *(const uint4*)(sa + lds_off(wm * TM + i * 16 + frow, ks * 4 + fchunk));
+        if constexpr (RELU) af = relu_pk16(af);
+        #pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
+      }
+    }
+  };
+
+  const int KT = p.K / BK;
+  issue(0, 0);
+  if (KT > 1) {
+    issue(1, 1);
+    wait_vmcnt<LT>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  lds_barrier();
+  for (int kt = 0; kt < KT; ++kt) {
+    compute(kt & 1);
+    lds_barrier();  // every wave is done reading stage kt&1
+    if (kt + 2 < KT) {
+      issue(kt + 2, kt & 1);
+      wait_vmcnt<LT>();  // tile kt+1 (issued one iteration ago) has landed
+    } else {
+      wait_vmcnt<0>();
+    }
+    lds_barrier();
+  }
+
+  const int em = lane & 15, en = 4 * (lane >> 4);
+  float hs = 0.f;
+  #pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * TM + i * 16 + em;
+    #pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * TN + j * 16 + en;
+      if (m < p.M && n < p.N) {
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        epilogue4<K_>(p, m, n, v, hs);
+      }
+    }
+  }
+}
+
+// ========================================================== small-tile engine
+constexpr int NT = 256;
 
 template <typename K_, int BM, int BN, int WM, int WN, bool CONV>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
@@ -67,27 +339,16 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
   const int tile_n = blockIdx.x % p.tiles_n;
   const int tile_m = blockIdx.x / p.tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int kc = tid & 7;        // 16-B chunk within a 64-wide K row
-  const int rbase = tid >> 3;    // first row of this thread's chunks (step 32)
+  const int kc = tid & 7;      // 16-B chunk within a 64-wide K row
+  const int rbase = tid >> 3;  // first row of this thread's chunks (step 32)
 
-  // ---- per-thread load descriptors
   const u16* a_ptr[CA];
-  int a_iy[CA], a_ix[CA], a_pix[CA];
+  ConvRow a_cr[CA];
   #pragma unroll
   for (int i = 0; i < CA; ++i) {
-    int m = m0 + rbase + 32 * i;
-    bool ok = m < p.M;
-    int mc = ok ? m : p.M - 1;
-    if constexpr (!CONV) {
-      a_ptr[i] = p.A + (long long)mc * p.lda + kc * 8;
-    } else {
-      int hw = p.out_h * p.out_w;
-      int b = mc / hw, r = mc - b * hw;
-      int oy = r / p.out_w, ox = r - oy * p.out_w;
-      a_iy[i] = ok ? oy * p.stride - p.pad : -(1 << 28);
-      a_ix[i] = ox * p.stride - p.pad;
-      a_pix[i] = b * p.in_h * p.in_w;
-    }
+    const int m = m0 + rbase + 32 * i;
+    if constexpr (!CONV) a_ptr[i] = p.A + (long long)(m < p.M ? m : p.M - 1) * p.lda + kc * 8;
+    else a_cr[i] = conv_row(p, m);
   }
   const u16* b_ptr[CB];
   #pragma unroll
@@ -98,7 +359,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
   }
 
   uint4 ra[CA], rb[CB];
-  // conv tap state (uniform): current (ky, kx, ci0) of the K tile being loaded
   int t_ky = 0, t_kx = 0, t_ci = 0;
 
   auto load_tile = [&](int k0) {
@@ -108,13 +368,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
     } else {
       #pragma unroll
       for (int i = 0; i < CA; ++i) {
-        int iy = a_iy[i] + t_ky, ix = a_ix[i] + t_kx;
-        bool inb = (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+        bool inb;
+        const u16* s = conv_src(p, a_cr[i], t_ky, t_kx, t_ci + kc * 8, inb);
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (inb) {
-          long long pix = (long long)a_pix[i] + (long long)iy * p.in_w + ix;
-          v = *(const uint4*)(p.A + pix * p.in_c + t_ci + kc * 8);
-        }
+        if (inb) v = *(const uint4*)s;
         ra[i] = v;
       }
       t_ci += BK;
@@ -175,13 +432,12 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds rows m = .. + (lane & 15), cols n = .. + 4*(lane >> 4) + r
+  // epilogue: lane holds rows m = .. + (lane & 15), cols n = .. + 4*(lane >> 4) + r
   const int em = lane & 15;
   const int en = 4 * (lane >> 4);
   float hsum[FM];
   #pragma unroll
   for (int i = 0; i < FM; ++i) hsum[i] = 0.f;
-
   #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wm * TM + i * 16 + em;
@@ -190,67 +446,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
       const int n = n0 + wn * TN + j * 16 + en;
       if (m >= p.M || n >= p.N) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.bias) {
-        float4 b = *(const float4*)(p.bias + n);
-        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-      }
-      if (p.act == DP_ACT_RELU) {
-        #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      } else if (p.act == DP_ACT_GELU) {
-        #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
-      }
-      if (p.gamma) {
-        float4 g = *(const float4*)(p.gamma + n);
-        v[0] *= g.x; v[1] *= g.y; v[2] *= g.z; v[3] *= g.w;
-      }
-      if (p.pos) {
-        const float* pp = p.pos + (long long)(m % p.pos_group + p.pos_off) * p.ldpos + n;
-        float4 q = *(const float4*)pp;
-        v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
-      }
-      if (p.R1) {
-        uint2 r = *(const uint2*)(p.R1 + (long long)m * p.ldr1 + n);
-        v[0] += K_::to_f(r.x & 0xffff); v[1] += K_::to_f(r.x >> 16);
-        v[2] += K_::to_f(r.y & 0xffff); v[3] += K_::to_f(r.y >> 16);
-      }
-      if (p.R2) {
-        uint2 r = *(const uint2*)(p.R2 + (long long)m * p.ldr2 + n);
-        v[0] += K_::to_f(r.x & 0xffff); v[1] += K_::to_f(r.x >> 16);
-        v[2] += K_::to_f(r.y & 0xffff); v[3] += K_::to_f(r.y >> 16);
-      }
-      if (p.head_w) {
-        float4 w = *(const float4*)(p.head_w + n);
-        hsum[i] += v[0] * w.x + v[1] * w.y + v[2] * w.z + v[3] * w.w;
-        continue;
-      }
-      long long off;
-      if (p.store_mode == DP_STORE_DECONV2X2) {
-        const int hw = p.dc_h * p.dc_w;
-        const int b = m / hw, rr = m - b * hw;
-        const int y = rr / p.dc_w, x = rr - y * p.dc_w;
-        const int q = n / p.dc_cout, co = n - q * p.dc_cout;
-        const long long pix = ((long long)b * 2 * p.dc_h + 2 * y + (q >> 1)) * (2 * p.dc_w) + 2 * x + (q & 1);
-        off = pix * p.ldc + co;
-      } else {
-        long long row = m;
-        if (p.row_group) row = (long long)(m / p.row_group) * p.row_group_out + p.row_off + m % p.row_group;
-        off = row * p.ldc + n;
-      }
-      if (p.c_dtype == DP_F32) {
-        float* c = (float*)p.C + off;
-        if (p.accumulate) {
-          float4 o = *(const float4*)c;
-          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-        }
-        *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        uint2 o;
-        o.x = (uint32_t)K_::from_f(v[0]) | ((uint32_t)K_::from_f(v[1]) << 16);
-        o.y = (uint32_t)K_::from_f(v[2]) | ((uint32_t)K_::from_f(v[3]) << 16);
-        *(uint2*)((u16*)p.C + off) = o;
-      }
+      epilogue4<K_>(p, m, n, v, hsum[i]);
     }
   }
   if (p.head_w) {
@@ -267,7 +463,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
 }
 
 template <typename K_, int BM, int BN, int WM, int WN>
-int launch_t(const GemmP& p0, bool conv, hipStream_t s) {
+int launch_small(const GemmP& p0, bool conv, hipStream_t s) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + BM - 1) / BM;
@@ -280,12 +476,32 @@ int launch_t(const GemmP& p0, bool conv, hipStream_t s) {
   return 0;
 }
 
+template <typename K_, int BN>
+int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_m = (p.M + 255) / 256;
+  dim3 grid(p.tiles_n * tiles_m);
+  if (conv && p.relu_a)
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, true, true>), grid, dim3(NT_BIG), 0, s, p);
+  else if (conv)
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, true, false>), grid, dim3(NT_BIG), 0, s, p);
+  else if (p.relu_a)
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, false, true>), grid, dim3(NT_BIG), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, false, false>), grid, dim3(NT_BIG), 0, s, p);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename K_>
 int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
   switch (tile) {
-    case DP_TILE_256x64: return launch_t<K_, 256, 64, 4, 1>(p, conv, s);
-    case DP_TILE_256x32: return launch_t<K_, 256, 32, 4, 1>(p, conv, s);
-    default: return launch_t<K_, 128, 128, 2, 2>(p, conv, s);
+    case DP_TILE_256x64: return launch_small<K_, 256, 64, 4, 1>(p, conv, s);
+    case DP_TILE_256x32: return launch_small<K_, 256, 32, 4, 1>(p, conv, s);
+    case DP_TILE_128x128: return launch_small<K_, 128, 128, 2, 2>(p, conv, s);
+    case DP_TILE_BIG_256x128: return launch_big<K_, 128>(p, conv, s);
+    default: return launch_big<K_, 256>(p, conv, s);
   }
 }
 
@@ -317,7 +533,17 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
     if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;
     tile = DP_TILE_256x32;
   }
-  if (tile == DP_TILE_AUTO) tile = a->N <= 32 ? DP_TILE_256x32 : (a->N <= 64 ? DP_TILE_256x64 : DP_TILE_128x128);
+  if (tile == DP_TILE_AUTO) {
+    if (a->N <= 32) tile = DP_TILE_256x32;
+    else if (a->N <= 64) tile = DP_TILE_256x64;
+    else {
+      // 256x256 halves operand traffic per FLOP but needs enough tiles to keep
+      // 256 CUs busy through the last wave of workgroups (measured crossover
+      // ~1200 tiles on the ViT / decoder shapes: tools/gemm_bench.py).
+      const long long tiles256 = (long long)((a->M + 255) / 256) * (a->N / 256);
+      tile = (a->N % 256 == 0 && tiles256 >= 1200) ? DP_TILE_BIG_256x256 : DP_TILE_BIG_256x128;
+    }
+  }
 
   GemmP p;
   p.M = a->M; p.N = a->N; p.K = a->K;

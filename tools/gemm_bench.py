@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Time dp_gemm tile engines on the Depth Pro GEMM shapes vs torch.matmul (hipBLASLt) on the same data."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
+from depth_pro import ops  # noqa: E402
+from depth_pro._lib import (DP_TILE_128x128, DP_TILE_BIG_256x128, DP_TILE_BIG_256x256)  # noqa: E402
+
+SHAPES = [  # (name, M, N, K, kw)
+    ("qkv", 20195, 3072, 1024, {}),
+    ("proj+res", 20195, 1024, 1024, {"acc": True}),
+    ("fc1+gelu", 20195, 4096, 1024, {"gelu": True}),
+    ("fc2+res", 20195, 1024, 4096, {"acc": True}),
+    ("conv3x3 768^2 256->256", 768 * 768, 256, 2304, {"conv": 768}),
+    ("conv3x3 384^2 256->256", 384 * 384, 256, 2304, {"conv": 384}),
+    ("head conv 768^2 256->128", 768 * 768, 128, 2304, {"conv": 768}),
+]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    dev = torch.device("cuda:0")
+    dt = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    for name, M, N, K, kw in SHAPES:
+        B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
+        bias = torch.randn(N, device=dev, generator=g)
+        if "conv" in kw:
+            S = kw["conv"]
+            cin = K // 9
+            A = torch.randn(S * S, cin, device=dev, generator=g).to(dt)
+            conv = dict(in_h=S, in_w=S, in_c=cin, k=3, stride=1, pad=1, out_h=S, out_w=S)
+        else:
+            A = torch.randn(M, K, device=dev, generator=g).to(dt)
+            conv = None
+        C = torch.zeros(M, N, device=dev, dtype=torch.float32 if kw.get("acc") else dt)
+        flop = 2.0 * M * N * K
+        res = []
+        for tname, tile in (("128x128", DP_TILE_128x128), ("big256x256", DP_TILE_BIG_256x256),
+                            ("big256x128", DP_TILE_BIG_256x128)):
+            if tile == DP_TILE_BIG_256x256 and N % 256:
+                continue
+            f = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, conv=conv, bias=bias, act=2 if kw.get("gelu") else 0,
+                                 accumulate=bool(kw.get("acc")), tile=tile)  # noqa: E731
+            ms = timeit(f)
+            res.append(f"{tname} {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
+        # correctness of the big engine vs the small one on this shape
+        if not kw.get("acc"):
+            C1 = torch.empty_like(C)
+            ops.gemm(A, B, C1, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_128x128)
+            C2 = torch.empty_like(C)
+            ops.gemm(A, B, C2, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_BIG_256x128)
+            d = (C1.float() - C2.float()).abs().max().item()
+            res.append(f"max|small-big|={d:.2e}")
+        if conv is None:
+            ms = timeit(lambda: torch.matmul(A, B.t()))
+            res.append(f"torch.matmul {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
+        print(f"{name:28s} " + " | ".join(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
