@@ -204,6 +204,7 @@ class Engine:
         self.f6 = e(6 * 6, 32)
         self.fov_deg = e(1, 1, 1, 1, dtype=torch.float32)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.side = torch.cuda.Stream(device=dev)
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
@@ -266,10 +267,33 @@ class Engine:
         return self.feats
 
     # -------------------------------------------------------------- forward
+    def _side_encoders(self):
+        """Image encoder (+ lowres upsample) and FOV encoder (+ Linear): ~5 % of the
+        frame's FLOPs at M = 577 rows, far too few tiles to fill 256 CUs alone, so
+        they run on a side stream and fill the patch encoder's idle CUs."""
+        P, e = self.P, "encoder."
+        self._vit("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
+        ops.merge_windows(self.vi.h, 0, 1, 0, self.g)
+        self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
+                     C_off=D, ldc=2 * D)
+        if self.use_fov:
+            vf = self.vf
+            self._vit("fov.encoder.0.", vf, 1, 34 * PTOK)
+            ops.gemm(vf.h, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
+
     def forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Run the network on `self.x0`; results in self.canonical / self.fov_deg."""
+        """Run the network on `self.x0`; results in self.canonical / self.fov_deg.
+
+        Two streams: the current stream runs the patch encoder -> decoder -> head;
+        `self.side` runs the image + FOV encoders (forked after the window
+        im2col, joined before fuse_lowres / the FOV head).
+        """
         P = self.P
+        main = torch.cuda.current_stream(self.dev)
         ops.patchify_pyramid(self.x0, self.cols)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            self._side_encoders()
         vp = self.vp
         hooks = {
             5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
@@ -279,8 +303,6 @@ class Engine:
         ops.merge_windows(vp.h, 0, 5, 3, self.f0)
         ops.merge_windows(vp.h, 25, 3, 6, self.f1)
         ops.merge_windows(vp.h, 34, 1, 0, self.f2)
-        self._vit("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
-        ops.merge_windows(self.vi.h, 0, 1, 0, self.g)
         # project / upsample (encoder.py:314-324)
         e = "encoder."
         ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
@@ -296,11 +318,16 @@ class Engine:
         self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
         ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
-        self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
-                     C_off=D, ldc=2 * D)
+        main.wait_stream(self.side)  # join: image-encoder half of `cat` and fov tokens ready
         ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
         self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)
+        if self.use_fov:  # FOV head (fov.py:56-82) only needs the lowres features
+            self._conv3(self.low, 48, 256, P["fov.down.w"], self.fx, 128, bias=P["fov.down.b"], act=DP_ACT_RELU,
+                        R1=self.fov_tok, stride=2)
+            self._conv3(self.fx, 24, 128, P["fov.h0.w"], self.f12, 64, bias=P["fov.h0.b"], act=DP_ACT_RELU, stride=2)
+            self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
+            ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
         f = self._fusion(4, self.low, 48, None)
         for i, (enc, s, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)), (1, (self.enc1, 384, 256))):
             c = self.dec[s]["c"]
@@ -312,16 +339,6 @@ class Engine:
         self._deconv(self.h0, 768, 128, P["head.1.w"], self.h1, 128, bias=P["head.1.b"])
         self._conv3(self.h1, 1536, 128, P["head.2.w"], self.canonical, 32, bias=P["head.2.b"], act=DP_ACT_RELU,
                     head_w=P["head.4.w"], head_b=P["head.4.b"])
-        # FOV (fov.py:56-82)
-        if self.use_fov:
-            vf = self.vf
-            self._vit("fov.encoder.0.", vf, 1, 34 * PTOK)
-            ops.gemm(vf.h, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
-            self._conv3(self.low, 48, 256, P["fov.down.w"], self.fx, 128, bias=P["fov.down.b"], act=DP_ACT_RELU,
-                        R1=self.fov_tok, stride=2)
-            self._conv3(self.fx, 24, 128, P["fov.h0.w"], self.f12, 64, bias=P["fov.h0.b"], act=DP_ACT_RELU, stride=2)
-            self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
-            ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
         return self.canonical, self.fov_deg
 
     # ---------------------------------------------------------------- graphs
