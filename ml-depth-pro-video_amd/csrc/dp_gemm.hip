@@ -54,7 +54,10 @@ struct GemmP {
   const float* head_w;
   float head_b;
   int tiles_n;
+  int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
 };
+
+int g_dbg_flags = 0;
 
 // 16 zero bytes x 8: source of the implicit-conv zero padding for LDS-DMA loads
 __device__ __attribute__((aligned(16))) uint32_t g_zero_page[32];
@@ -131,6 +134,69 @@ __device__ __forceinline__ void epilogue4(const GemmP& p, int m, int n, float (&
   }
 }
 
+// Same epilogue for 8 consecutive columns n..n+7 (N % 8 == 0 on this path):
+// 16-32 B loads and stores per lane.
+template <typename K_>
+__device__ __forceinline__ void add8_16(float (&v)[8], const u16* p) {
+  const uint4 r = *(const uint4*)p;
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  #pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] += K_::to_f(w[k] & 0xffff);
+    v[2 * k + 1] += K_::to_f(w[k] >> 16);
+  }
+}
+__device__ __forceinline__ void add8_f32(float (&v)[8], const float* p) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+  v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+}
+template <typename K_>
+__device__ __forceinline__ void epilogue8(const GemmP& p, int m, int n, float (&v)[8]) {
+  if (p.bias) add8_f32(v, p.bias + n);
+  if (p.act == DP_ACT_RELU) {
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
+  } else if (p.act == DP_ACT_GELU) {
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = gelu_erf(v[r]);
+  }
+  if (p.gamma) {
+    const float4 a = *(const float4*)(p.gamma + n), b = *(const float4*)(p.gamma + n + 4);
+    v[0] *= a.x; v[1] *= a.y; v[2] *= a.z; v[3] *= a.w;
+    v[4] *= b.x; v[5] *= b.y; v[6] *= b.z; v[7] *= b.w;
+  }
+  if (p.pos) add8_f32(v, p.pos + (long long)(m % p.pos_group + p.pos_off) * p.ldpos + n);
+  if (p.R1) add8_16<K_>(v, p.R1 + (long long)m * p.ldr1 + n);
+  if (p.R2) add8_16<K_>(v, p.R2 + (long long)m * p.ldr2 + n);
+  long long off;
+  if (p.store_mode == DP_STORE_DECONV2X2) {
+    const int hw = p.dc_h * p.dc_w;
+    const int b = m / hw, rr = m - b * hw;
+    const int y = rr / p.dc_w, x = rr - y * p.dc_w;
+    const int q = n / p.dc_cout, co = n - q * p.dc_cout;
+    const long long pix = ((long long)b * 2 * p.dc_h + 2 * y + (q >> 1)) * (2 * p.dc_w) + 2 * x + (q & 1);
+    off = pix * p.ldc + co;
+  } else {
+    long long row = m;
+    if (p.row_group) row = (long long)(m / p.row_group) * p.row_group_out + p.row_off + m % p.row_group;
+    off = row * p.ldc + n;
+  }
+  if (p.c_dtype == DP_F32) {
+    float* c = (float*)p.C + off;
+    if (p.accumulate) add8_f32(v, c);
+    *(float4*)c = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    uint4 o;
+    o.x = (uint32_t)K_::from_f(v[0]) | ((uint32_t)K_::from_f(v[1]) << 16);
+    o.y = (uint32_t)K_::from_f(v[2]) | ((uint32_t)K_::from_f(v[3]) << 16);
+    o.z = (uint32_t)K_::from_f(v[4]) | ((uint32_t)K_::from_f(v[5]) << 16);
+    o.w = (uint32_t)K_::from_f(v[6]) | ((uint32_t)K_::from_f(v[7]) << 16);
+    *(uint4*)((u16*)p.C + off) = o;
+  }
+}
+
 // implicit-conv row descriptor: output pixel m -> top-left input tap
 struct ConvRow {
   int iy, ix, pix;
@@ -182,18 +248,44 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
       : "memory");
 }
 
-template <typename K_, int BN, bool CONV, bool RELU>
+// LDS image of one operand tile: rows of BKT 16-bit elements (64 or 128 B), the
+// 16-B chunk index XOR-swizzled so that the 16 rows one ds_read_b128 lane group
+// reads hit 16 distinct bank slots (conflict-free, checked with SQ_LDS_BANK_CONFLICT).
+template <int BKT>
+__device__ __forceinline__ int lds_off_t(int row, int chunk) {
+  if constexpr (BKT == 64) return row * 64 + ((chunk ^ (row & 7)) << 3);
+  else return row * 32 + ((chunk ^ ((row >> 1) & 3)) << 3);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n <= N, n a multiple of step
+  if constexpr (N == 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N) wait_vmcnt<N>();
+    else wait_vmcnt_le<N - 1>(n);
+  }
+}
+
+template <typename K_, int BN, int BKT, int NS, bool CONV, bool RELU>
 __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   constexpr int BM = 256;
   constexpr int WN = 4;
   constexpr int TM = 128, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int RB = BKT * 2;                 // LDS row bytes
+  constexpr int CR = BKT / 8;                 // 16-B chunks per row
+  constexpr int ROWS_PER_WAVE_PIECE = 1024 / RB;
+  constexpr int ROWS_PER_ROUND = 8 * ROWS_PER_WAVE_PIECE;  // rows covered by one piece of every wave
+  constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int LA = BM * 8 / NT_BIG;  // 16-B LDS-DMA pieces per thread per A tile (4)
-  constexpr int LB = BN * 8 / NT_BIG;  // per B tile (4 or 2)
+  constexpr int LA = BM / ROWS_PER_ROUND;     // LDS-DMA pieces per thread per A tile
+  constexpr int LB = BN / ROWS_PER_ROUND;
   constexpr int LT = LA + LB;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  constexpr int EPI_BYTES = 8 * 32 * (TN + 4) * 4;  // epilogue staging (8 waves x 32 fp32 rows)
+  constexpr int SMEM = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
+  static_assert(NS >= 2 && SMEM <= 160 * 1024 && LB >= 1, "LDS ring");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6;
@@ -207,15 +299,16 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  // LDS-DMA piece i of this thread: tile row i*64 + wave*8 + lane/8, LDS slot lane%8 holds
-  // logical chunk (lane%8) ^ (row&7) -> the swizzle is applied on the SOURCE address.
-  const int prow = wave * 8 + (lane >> 3);
-  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  // LDS-DMA piece i of this thread covers tile row i*ROWS_PER_ROUND + wave*ROWS_PER_WAVE_PIECE + lane/CR;
+  // LDS slot lane%CR of that row holds logical chunk (lane%CR) ^ swz(row): the swizzle is
+  // applied on the SOURCE address, the LDS image stays lane-linear.
+  const int prow = wave * ROWS_PER_WAVE_PIECE + lane / CR;
+  const int pchunk = BKT == 64 ? ((lane & 7) ^ ((lane >> 3) & 7)) : ((lane & 3) ^ ((lane >> 3) & 3));
   const u16* a_src[LA];
   ConvRow a_cr[LA];
   #pragma unroll
   for (int i = 0; i < LA; ++i) {
-    const int m = m0 + i * 64 + prow;
+    const int m = m0 + i * ROWS_PER_ROUND + prow;
     if constexpr (CONV) {
       a_cr[i] = conv_row(p, m);
     } else {
@@ -225,7 +318,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   const u16* b_src[LB];
   #pragma unroll
   for (int i = 0; i < LB; ++i) {
-    const int n = n0 + i * 64 + prow;
+    const int n = n0 + i * ROWS_PER_ROUND + prow;
     b_src[i] = p.B + (long long)(n < p.N ? n : p.N - 1) * p.ldb + pchunk * 8;
   }
   int t_ky = 0, t_kx = 0, t_ci = 0;  // conv tap of the next K tile to issue (uniform)
@@ -234,7 +327,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   auto issue = [&](int kt, int stage) {
     const uint32_t sa = lds_base + stage * STAGE;
     const uint32_t sb = sa + A_BYTES;
-    const int k0 = kt * BK;
+    const int k0 = kt * BKT;
     #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const void* src;
@@ -248,7 +341,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       glds16(src, sa + i * 8192);
     }
     if constexpr (CONV) {
-      t_ci += BK;
+      t_ci += BKT;
       if (t_ci == p.in_c) {
         t_ci = 0;
         if (++t_kx == p.k_w) { t_kx = 0; ++t_ky; }
@@ -265,57 +358,98 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15, fchunk = lane >> 4;
+  constexpr int KS = BKT / 32;
+  // Fragment reads for the whole step are issued up front (all FM+FN per k-sub-step),
+  // so the LDS latency of sub-step ks+1 hides under the MFMAs of sub-step ks.
   auto compute = [&](int stage) {
     const u16* sa = (const u16*)(smem + stage * STAGE);
     const u16* sb = (const u16*)(smem + stage * STAGE + A_BYTES);
+    uint4 af[KS][FM], bf[KS][FN];
     #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      uint4 bf[FN];
+    for (int ks = 0; ks < KS; ++ks) {
       #pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = *(const uint4*)(sb + lds_off(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      for (int j = 0; j < FN; ++j)
+        bf[ks][j] = *(const uint4*)(sb + lds_off_t<BKT>(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      #pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[ks][i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
+    }
+    #pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      __builtin_amdgcn_s_setprio(1);
       #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        uint4 af = *(const uint4*)(sa + lds_off(wm * TM + i * 16 + frow, ks * 4 + fchunk));
-        if constexpr (RELU) af = relu_pk16(af);
+        uint4 a = af[ks][i];
+        if constexpr (RELU) a = relu_pk16(a);
         #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
+        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[ks][j], a, acc[i][j]);
       }
+      __builtin_amdgcn_s_setprio(0);
     }
   };
 
-  const int KT = p.K / BK;
-  issue(0, 0);
-  if (KT > 1) {
-    issue(1, 1);
-    wait_vmcnt<LT>();
-  } else {
-    wait_vmcnt<0>();
-  }
-  lds_barrier();
+  // NS-stage ring, one barrier per K step.  Top of iteration kt: tiles
+  // kt .. kt+NS-2 are in flight; wait (counted) until this thread's pieces of
+  // tile kt landed, then the barrier makes tile kt visible to every wave AND
+  // certifies that every wave finished compute(kt-1), whose stage is refilled
+  // with tile kt+NS-1 right away -- NS-1 steps of MFMA work cover each load.
+  const int KT = p.K / BKT;
+  #pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < KT) issue(t, t);
+  int stage = 0;
   for (int kt = 0; kt < KT; ++kt) {
-    compute(kt & 1);
-    lds_barrier();  // every wave is done reading stage kt&1
-    if (kt + 2 < KT) {
-      issue(kt + 2, kt & 1);
-      wait_vmcnt<LT>();  // tile kt+1 (issued one iteration ago) has landed
-    } else {
-      wait_vmcnt<0>();
-    }
+    const int after = min(NS - 2, KT - 1 - kt);  // steps issued after kt, allowed to stay in flight
+    wait_vmcnt_le<(NS - 2) * LT>(after * LT);
     lds_barrier();
+    if (kt + NS - 1 < KT && !(p.dbg & 2)) {
+      int st = stage + NS - 1;
+      st = st >= NS ? st - NS : st;
+      issue(kt + NS - 1, st);
+    }
+    if (p.dbg & 4) {
+      const u16* sa = (const u16*)(smem + stage * STAGE);
+      uint4 t = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + frow, fchunk));
+      asm volatile("" ::"v"(t.x));
+    } else {
+      compute(stage);
+    }
+    stage = stage + 1 == NS ? 0 : stage + 1;
   }
 
-  const int em = lane & 15, en = 4 * (lane >> 4);
-  float hs = 0.f;
-  #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = m0 + wm * TM + i * 16 + em;
+  if (p.dbg & 1) {
     #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * TN + j * 16 + en;
-      if (m < p.M && n < p.N) {
-        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        epilogue4<K_>(p, m, n, v, hs);
-      }
+    for (int i = 0; i < FM; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j][0]), "v"(acc[i][j][1]), "v"(acc[i][j][2]), "v"(acc[i][j][3]));
+    return;
+  }
+  // Epilogue through LDS: the MFMA layout gives each lane 4 columns of one row
+  // (16 rows x 32-64 B per store instruction -- partial cache lines, measured at
+  // ~half of the kernel's time on the ViT shapes).  Each wave instead parks 32
+  // rows of its fp32 tile in a private LDS slab and reads them back row-major,
+  // so every lane owns 8 consecutive columns and a store instruction writes
+  // whole 128-256 B row segments.
+  lds_barrier();  // the ring is free once every wave has left the K loop
+  constexpr int SROW = TN + 4;                // fp32 row stride (bank-conflict-free writes)
+  constexpr int CPR = TN / 8;                 // 8-column chunks per row
+  constexpr int RPI = 64 / CPR;               // rows per read instruction
+  float* stg = (float*)smem + wave * (32 * SROW);
+  #pragma unroll
+  for (int q = 0; q < FM / 2; ++q) {          // 32 rows (two 16-row fragments) per pass
+    #pragma unroll
+    for (int i = 0; i < 2; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j)
+        *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[2 * q + i][j];
+    #pragma unroll
+    for (int r0 = 0; r0 < 32; r0 += RPI) {
+      const int row = r0 + lane / CPR, c8 = (lane % CPR) * 8;
+      const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
+      const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const int m = m0 + wm * TM + q * 32 + row, n = n0 + wn * TN + c8;
+      if (m < p.M && n < p.N) epilogue8<K_>(p, m, n, v);
     }
   }
 }
@@ -476,20 +610,21 @@ int launch_small(const GemmP& p0, bool conv, hipStream_t s) {
   return 0;
 }
 
-template <typename K_, int BN>
+template <typename K_, int BN, int BKT>
 int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + 255) / 256;
   dim3 grid(p.tiles_n * tiles_m);
+  constexpr int NS = (160 * 1024) / ((256 + BN) * BKT * 2) > 6 ? 6 : (160 * 1024) / ((256 + BN) * BKT * 2);
   if (conv && p.relu_a)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, true, true>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, true, true>), grid, dim3(NT_BIG), 0, s, p);
   else if (conv)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, true, false>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, true, false>), grid, dim3(NT_BIG), 0, s, p);
   else if (p.relu_a)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, false, true>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, false, true>), grid, dim3(NT_BIG), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, false, false>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, false, false>), grid, dim3(NT_BIG), 0, s, p);
   DP_CHECK_LAUNCH();
   return 0;
 }
@@ -500,12 +635,20 @@ int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
     case DP_TILE_256x64: return launch_small<K_, 256, 64, 4, 1>(p, conv, s);
     case DP_TILE_256x32: return launch_small<K_, 256, 32, 4, 1>(p, conv, s);
     case DP_TILE_128x128: return launch_small<K_, 128, 128, 2, 2>(p, conv, s);
-    case DP_TILE_BIG_256x128: return launch_big<K_, 128>(p, conv, s);
-    default: return launch_big<K_, 256>(p, conv, s);
+    case DP_TILE_BIG_256x128: return launch_big<K_, 128, 64>(p, conv, s);
+    case DP_TILE_BIG_256x128_K32: return launch_big<K_, 128, 32>(p, conv, s);
+    case DP_TILE_BIG_256x256_K32: return launch_big<K_, 256, 32>(p, conv, s);
+    default: return launch_big<K_, 256, 64>(p, conv, s);
   }
 }
 
 }  // namespace
+
+// Not part of the ABI header: ablation switches for the GEMM microbenchmark only.
+extern "C" int dp_gemm_debug_flags(int flags) {
+  g_dbg_flags = flags;
+  return 0;
+}
 
 extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
   if (!a) return DP_ERR_ARG;
@@ -536,14 +679,17 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
   if (tile == DP_TILE_AUTO) {
     if (a->N <= 32) tile = DP_TILE_256x32;
     else if (a->N <= 64) tile = DP_TILE_256x64;
+    else if (a->N % 8 != 0) tile = DP_TILE_128x128;
     else {
       // 256x256 halves operand traffic per FLOP but needs enough tiles to keep
       // 256 CUs busy through the last wave of workgroups (measured crossover
-      // ~1200 tiles on the ViT / decoder shapes: tools/gemm_bench.py).
+      // ~500 tiles on the ViT / decoder shapes: tools/gemm_bench.py).
       const long long tiles256 = (long long)((a->M + 255) / 256) * (a->N / 256);
-      tile = (a->N % 256 == 0 && tiles256 >= 1200) ? DP_TILE_BIG_256x256 : DP_TILE_BIG_256x128;
+      tile = (a->N % 256 == 0 && tiles256 >= 500) ? DP_TILE_BIG_256x256 : DP_TILE_BIG_256x128;
     }
   }
+
+  if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
 
   GemmP p;
   p.M = a->M; p.N = a->N; p.K = a->K;
@@ -560,6 +706,7 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
   p.row_group = a->row_group; p.row_group_out = a->row_group_out; p.row_off = a->row_off;
   p.head_w = a->head_w; p.head_b = a->head_b;
   p.tiles_n = 1;
+  p.dbg = g_dbg_flags;
   hipStream_t s = (hipStream_t)stream;
   const bool conv = a->a_mode == DP_A_CONV;
   if (a->dtype == DP_BF16) return launch_k<KBF16>(p, tile, conv, s);

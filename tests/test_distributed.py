@@ -1,0 +1,80 @@
+"""Frame-parallel plumbing over torch.distributed (gloo, world_size 2, CPU).
+
+Covers depth_pro.distributed: round-robin frame sharding, the one-blob packed
+weight broadcast and the depth-map gather, exactly as bench.py / the frame loop
+use them over RCCL on GPUs.
+"""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from depth_pro import distributed as D
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        packed = None
+        if rank == 0:
+            g = torch.Generator().manual_seed(0)
+            packed = {"a.w": torch.randn(7, 5, generator=g).to(torch.bfloat16),
+                      "b.b": torch.randn(13, generator=g),
+                      "c.s": 0.25, "d.w": torch.randn(3, 64, generator=g).half()}
+        got = D.broadcast_packed(packed, torch.device("cpu"), src=0)
+        g = torch.Generator().manual_seed(0)
+        ref = {"a.w": torch.randn(7, 5, generator=g).to(torch.bfloat16), "b.b": torch.randn(13, generator=g),
+               "c.s": 0.25, "d.w": torch.randn(3, 64, generator=g).half()}
+        ok_bcast = all((torch.equal(got[k], ref[k]) and got[k].dtype == ref[k].dtype) if torch.is_tensor(ref[k])
+                       else got[k] == ref[k] for k in ref)
+        frames = D.shard_frames(10, rank, world)
+        per_step = []
+        for k in frames[:4]:
+            depth = torch.full((4, 6), float(k))  # stand-in for frame k's depth map
+            out = D.gather_frames(depth, dst=0)
+            if rank == 0:
+                per_step.append(out)
+        if rank == 0:
+            order = [int(t[0, 0].item()) for t in D.order_results(per_step, world)]
+            q.put(("order", order))
+        q.put(("rank", rank, frames, ok_bcast))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frame_sharding_broadcast_gather_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    msgs = [q.get(timeout=5) for _ in range(world + 1)]
+    ranks = {m[1]: m for m in msgs if m[0] == "rank"}
+    assert ranks[0][2] == [0, 2, 4, 6, 8] and ranks[1][2] == [1, 3, 5, 7, 9]
+    assert ranks[0][3] and ranks[1][3]
+    order = [m[1] for m in msgs if m[0] == "order"][0]
+    assert order == list(range(8))  # stream order restored at rank 0
+
+
+def test_shard_frames_covers_stream_once():
+    for world in (1, 2, 3, 8):
+        seen = sorted(k for r in range(world) for k in D.shard_frames(1024, r, world))
+        assert seen == list(range(1024))
+        assert all(D.frame_owner(k, world) == k % world for k in range(50))

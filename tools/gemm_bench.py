@@ -7,7 +7,8 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
 from depth_pro import ops  # noqa: E402
-from depth_pro._lib import (DP_TILE_128x128, DP_TILE_BIG_256x128, DP_TILE_BIG_256x256)  # noqa: E402
+from depth_pro._lib import (DP_TILE_128x128, DP_TILE_BIG_256x128, DP_TILE_BIG_256x128_K32,  # noqa: E402
+                            DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32)
 
 SHAPES = [  # (name, M, N, K, kw)
     ("qkv", 20195, 3072, 1024, {}),
@@ -34,10 +35,20 @@ def timeit(fn, iters=20):
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None, help="substring of one shape name")
+    ap.add_argument("--tile", default=None, help="128x128 | big256x256 | big256x128")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--ablate", action="store_true", help="time the no-store / no-load / no-mfma variants")
+    args = ap.parse_args()
     dev = torch.device("cuda:0")
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     for name, M, N, K, kw in SHAPES:
+        if args.only and args.only not in name:
+            continue
         B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
         bias = torch.randn(N, device=dev, generator=g)
         if "conv" in kw:
@@ -51,23 +62,37 @@ def main():
         C = torch.zeros(M, N, device=dev, dtype=torch.float32 if kw.get("acc") else dt)
         flop = 2.0 * M * N * K
         res = []
-        for tname, tile in (("128x128", DP_TILE_128x128), ("big256x256", DP_TILE_BIG_256x256),
-                            ("big256x128", DP_TILE_BIG_256x128)):
-            if tile == DP_TILE_BIG_256x256 and N % 256:
+        for tname, tile in (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
+                            ("b256x256k32", DP_TILE_BIG_256x256_K32), ("b256x128k32", DP_TILE_BIG_256x128_K32)):
+            if tile in (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32) and N % 256:
+                continue
+            if args.tile and args.tile != tname:
                 continue
             f = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, conv=conv, bias=bias, act=2 if kw.get("gelu") else 0,
                                  accumulate=bool(kw.get("acc")), tile=tile)  # noqa: E731
-            ms = timeit(f)
+            ms = timeit(f, args.iters)
             res.append(f"{tname} {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
+            if args.ablate and tname.startswith("big"):
+                from depth_pro import _lib
+                parts = []
+                for flags, lab in ((1, "nostore"), (2, "noload"), (3, "nostore+noload"), (4, "nomfma"), (5, "nomfma+nostore")):
+                    _lib.load().dp_gemm_debug_flags(flags)
+                    parts.append(f"{lab} {timeit(f, args.iters)*1e3:.1f}")
+                _lib.load().dp_gemm_debug_flags(0)
+                res.append("[" + " ".join(parts) + "]")
         # correctness of the big engine vs the small one on this shape
-        if not kw.get("acc"):
+        if not kw.get("acc") and not args.tile:
             C1 = torch.empty_like(C)
             ops.gemm(A, B, C1, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_128x128)
             C2 = torch.empty_like(C)
-            ops.gemm(A, B, C2, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_BIG_256x128)
-            d = (C1.float() - C2.float()).abs().max().item()
+            d = 0.0
+            for t in (DP_TILE_BIG_256x128, DP_TILE_BIG_256x128_K32, DP_TILE_BIG_256x256_K32):
+                if t == DP_TILE_BIG_256x256_K32 and N % 256:
+                    continue
+                ops.gemm(A, B, C2, M=M, N=N, K=K, conv=conv, bias=bias, tile=t)
+                d = max(d, (C1.float() - C2.float()).abs().max().item())
             res.append(f"max|small-big|={d:.2e}")
-        if conv is None:
+        if conv is None and not args.tile:
             ms = timeit(lambda: torch.matmul(A, B.t()))
             res.append(f"torch.matmul {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
         print(f"{name:28s} " + " | ".join(res), flush=True)
