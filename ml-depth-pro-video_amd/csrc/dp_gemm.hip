@@ -359,62 +359,131 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
 
   const int frow = lane & 15, fchunk = lane >> 4;
   constexpr int KS = BKT / 32;
-  // Fragment reads for the whole step are issued up front (all FM+FN per k-sub-step),
-  // so the LDS latency of sub-step ks+1 hides under the MFMAs of sub-step ks.
   auto compute = [&](int stage) {
     const u16* sa = (const u16*)(smem + stage * STAGE);
     const u16* sb = (const u16*)(smem + stage * STAGE + A_BYTES);
-    uint4 af[KS][FM], bf[KS][FN];
     #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
+      uint4 bf[FN];
       #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bf[ks][j] = *(const uint4*)(sb + lds_off_t<BKT>(wn * TN + j * 16 + frow, ks * 4 + fchunk));
-      #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        af[ks][i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
-    }
-    #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+        bf[j] = *(const uint4*)(sb + lds_off_t<BKT>(wn * TN + j * 16 + frow, ks * 4 + fchunk));
       __builtin_amdgcn_s_setprio(1);
       #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        uint4 a = af[ks][i];
-        if constexpr (RELU) a = relu_pk16(a);
+        uint4 af = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
+        if constexpr (RELU) af = relu_pk16(af);
         #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[ks][j], a, acc[i][j]);
+        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
       }
       __builtin_amdgcn_s_setprio(0);
     }
   };
 
-  // NS-stage ring, one barrier per K step.  Top of iteration kt: tiles
-  // kt .. kt+NS-2 are in flight; wait (counted) until this thread's pieces of
-  // tile kt landed, then the barrier makes tile kt visible to every wave AND
-  // certifies that every wave finished compute(kt-1), whose stage is refilled
-  // with tile kt+NS-1 right away -- NS-1 steps of MFMA work cover each load.
   const int KT = p.K / BKT;
-  #pragma unroll
-  for (int t = 0; t < NS - 1; ++t)
-    if (t < KT) issue(t, t);
-  int stage = 0;
-  for (int kt = 0; kt < KT; ++kt) {
-    const int after = min(NS - 2, KT - 1 - kt);  // steps issued after kt, allowed to stay in flight
-    wait_vmcnt_le<(NS - 2) * LT>(after * LT);
+  if constexpr (NS == 2) {
+    // 2-stage ring, one barrier per K step.  Top of iteration kt: tile kt is in
+    // flight; wait for it, then the barrier makes it visible to every wave AND
+    // certifies that every wave finished compute(kt-1), whose stage is refilled
+    // with tile kt+1 right away -- one step of MFMA work covers each load.
+    issue(0, 0);
+    int stage = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+      wait_vmcnt<0>();
+      lds_barrier();
+      if (kt + 1 < KT && !(p.dbg & 2)) issue(kt + 1, stage ^ 1);
+      if (p.dbg & 4) {
+        const u16* sa = (const u16*)(smem + stage * STAGE);
+        uint4 t = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + frow, fchunk));
+        asm volatile("" ::"v"(t.x));
+      } else {
+        compute(stage);
+      }
+      stage ^= 1;
+    }
+  } else {
+    // NS >= 3: software-pipelined.  The fragments of the next k sub-step (or of
+    // the next K step's first sub-step, once its tile is visible) are read from
+    // LDS while the MFMAs of the current sub-step run, alternating between two
+    // register sets; one barrier per K step, NS-2 steps of loads in flight.
+    uint4 fa0[FM], fb0[FN], fa1[FM], fb1[FN];
+    auto rd = [&](uint4 (&fa)[FM], uint4 (&fb)[FN], int stg, int ks) {
+      const u16* sa = (const u16*)(smem + stg * STAGE);
+      const u16* sb = (const u16*)(smem + stg * STAGE + A_BYTES);
+      #pragma unroll
+      for (int j = 0; j < FN; ++j)
+        fb[j] = *(const uint4*)(sb + lds_off_t<BKT>(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      #pragma unroll
+      for (int i = 0; i < FM; ++i)
+        fa[i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
+    };
+    auto mma = [&](const uint4 (&fa)[FM], const uint4 (&fb)[FN]) {
+      __builtin_amdgcn_s_setprio(1);
+      #pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        uint4 a = fa[i];
+        if constexpr (RELU) a = relu_pk16(a);
+        #pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(fb[j], a, acc[i][j]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto nxt = [&](int st) { return st + 1 == NS ? 0 : st + 1; };
+    // wait until tile t has landed: tiles issued so far are 0 .. min(KT-1, t+NS-2)
+    auto wait_tile = [&](int t) { wait_vmcnt_le<(NS - 2) * LT>(min(NS - 2, KT - 1 - t) * LT); };
+    #pragma unroll
+    for (int t = 0; t < NS - 1; ++t)
+      if (t < KT) issue(t, t);
+    wait_tile(0);
     lds_barrier();
-    if (kt + NS - 1 < KT && !(p.dbg & 2)) {
-      int st = stage + NS - 1;
-      st = st >= NS ? st - NS : st;
-      issue(kt + NS - 1, st);
-    }
-    if (p.dbg & 4) {
-      const u16* sa = (const u16*)(smem + stage * STAGE);
-      uint4 t = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + frow, fchunk));
-      asm volatile("" ::"v"(t.x));
+    rd(fa0, fb0, 0, 0);
+    int stage = 0;
+    if constexpr (KS == 2) {
+      for (int kt = 0; kt < KT; ++kt) {
+        if (kt + NS - 1 < KT) {
+          int st = stage + NS - 1;
+          issue(kt + NS - 1, st >= NS ? st - NS : st);
+        }
+        rd(fa1, fb1, stage, 1);
+        mma(fa0, fb0);
+        const int nst = nxt(stage);
+        if (kt + 1 < KT) {
+          wait_tile(kt + 1);
+          lds_barrier();
+          rd(fa0, fb0, nst, 0);
+        }
+        mma(fa1, fb1);
+        stage = nst;
+      }
     } else {
-      compute(stage);
+      for (int kt = 0; kt < KT; kt += 2) {
+        if (kt + NS - 1 < KT) {
+          int st = stage + NS - 1;
+          issue(kt + NS - 1, st >= NS ? st - NS : st);
+        }
+        int nst = nxt(stage);
+        if (kt + 1 < KT) {
+          wait_tile(kt + 1);
+          lds_barrier();
+          rd(fa1, fb1, nst, 0);
+        }
+        mma(fa0, fb0);
+        stage = nst;
+        if (kt + 1 >= KT) break;
+        if (kt + NS < KT) {
+          int st = stage + NS - 1;
+          issue(kt + NS, st >= NS ? st - NS : st);
+        }
+        nst = nxt(stage);
+        if (kt + 2 < KT) {
+          wait_tile(kt + 2);
+          lds_barrier();
+          rd(fa0, fb0, nst, 0);
+        }
+        mma(fa1, fb1);
+        stage = nst;
+      }
     }
-    stage = stage + 1 == NS ? 0 : stage + 1;
   }
 
   if (p.dbg & 1) {
@@ -616,7 +685,10 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   p.tiles_n = (p.N + BN - 1) / BN;
   const int tiles_m = (p.M + 255) / 256;
   dim3 grid(p.tiles_n * tiles_m);
-  constexpr int NS = (160 * 1024) / ((256 + BN) * BKT * 2) > 6 ? 6 : (160 * 1024) / ((256 + BN) * BKT * 2);
+  // ring depth: as deep as LDS allows for 256x128 (software-pipelined loop); the
+  // 256x256 tile keeps 2 stages (its double fragment set would not fit 256 VGPRs)
+  constexpr int NS_MAX = (160 * 1024) / ((256 + BN) * BKT * 2) > 6 ? 6 : (160 * 1024) / ((256 + BN) * BKT * 2);
+  constexpr int NS = BN == 256 ? 2 : NS_MAX;
   if (conv && p.relu_a)
     hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, true, true>), grid, dim3(NT_BIG), 0, s, p);
   else if (conv)
@@ -683,9 +755,9 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
     else {
       // 256x256 halves operand traffic per FLOP but needs enough tiles to keep
       // 256 CUs busy through the last wave of workgroups (measured crossover
-      // ~500 tiles on the ViT / decoder shapes: tools/gemm_bench.py).
+      // ~600 tiles on the ViT / decoder shapes: tools/gemm_bench.py).
       const long long tiles256 = (long long)((a->M + 255) / 256) * (a->N / 256);
-      tile = (a->N % 256 == 0 && tiles256 >= 500) ? DP_TILE_BIG_256x256 : DP_TILE_BIG_256x128;
+      tile = (a->N % 256 == 0 && tiles256 >= 600) ? DP_TILE_BIG_256x256 : DP_TILE_BIG_256x128;
     }
   }
 
