@@ -5,7 +5,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "ml-depth-pro-video_amd")
-for p in (PKG, REPO):
+for p in (REPO, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 

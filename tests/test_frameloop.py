@@ -1,0 +1,58 @@
+"""The generate_depth_maps drop-in: writers pinned to the reference colorize_depth (CPU),
+and the pipelined directory loop on the GPU."""
+
+import os
+
+import numpy as np
+import pytest
+
+import generate_depth_maps as G
+
+
+def test_colorize_matches_reference(golden_dir):
+    g = np.load(f"{golden_dir}/golden_frameloop.npz")
+    for cmap in ("turbo", "viridis", "jet"):
+        assert np.array_equal(G.colorize_depth(g["depth"], cmap=cmap), g[f"color_{cmap}"]), cmap
+    d = np.nan_to_num(g["depth"], nan=1.0)
+    assert np.array_equal(G.raw_depth_u16(d), g["raw_u16"])
+
+
+def test_png_writers_roundtrip(tmp_path):
+    from PIL import Image
+
+    rgb = (np.arange(48 * 64 * 3) % 251).astype(np.uint8).reshape(48, 64, 3)
+    G._write_png(str(tmp_path / "c.png"), rgb)
+    assert np.array_equal(np.asarray(Image.open(tmp_path / "c.png")), rgb)
+    u16 = (np.arange(48 * 64) * 20).astype(np.uint16).reshape(48, 64)
+    G._write_png(str(tmp_path / "r.png"), u16)
+    assert np.array_equal(np.asarray(Image.open(tmp_path / "r.png")).astype(np.uint16), u16)
+
+
+@pytest.mark.gpu
+def test_batch_loop_on_gpu(tmp_path, cuda):
+    from PIL import Image
+
+    import torch
+
+    src = tmp_path / "frames"
+    src.mkdir()
+    rng = np.random.default_rng(0)
+    for k in range(3):
+        Image.fromarray(rng.integers(0, 256, (360, 640, 3), dtype=np.uint8)).save(src / f"output_{k:04d}.png")
+    out = tmp_path / "depth"
+    n = G.batch_generate_depth_maps(str(src), str(out), pattern="output_*.png")
+    assert n == 3
+    files = sorted(os.listdir(out))
+    assert files == [f"output_{k:04d}_depth.png" for k in range(3)]
+    img = np.asarray(Image.open(out / files[0]))
+    assert img.shape == (360, 640, 3) and img.dtype == np.uint8
+    # the colored PNG is exactly colorize_depth(model.infer(...)) of the same frame
+    model, transform = G._model(cuda, False)
+    frame = np.asarray(Image.open(src / "output_0000.png"))
+    with torch.no_grad():
+        depth = model.infer(transform(frame))["depth"].cpu().numpy()
+    assert np.array_equal(img, G.colorize_depth(depth))
+    n_raw = G.batch_generate_depth_maps(str(src), str(tmp_path / "raw"), pattern="output_*.png", colored=False)
+    assert n_raw == 3
+    raw = np.asarray(Image.open(tmp_path / "raw" / "output_0001_depth.png"))
+    assert raw.shape == (360, 640)

@@ -43,7 +43,10 @@ def main(path, title=""):
     busy = 0.0
     for r in f:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        key = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])))
+        wg = (int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))) * \
+            (int(r["Grid_Size_Y"]) // max(1, int(r["Workgroup_Size_Y"]))) * \
+            (int(r["Grid_Size_Z"]) // max(1, int(r["Workgroup_Size_Z"])))
+        key = (short(r["Kernel_Name"]), wg)
         groups[key][0] += 1
         groups[key][1] += d
         busy += d
