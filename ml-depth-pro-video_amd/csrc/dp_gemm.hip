@@ -59,6 +59,34 @@ struct GemmP {
 
 int g_dbg_flags = 0;
 
+#ifdef DP_STAMPS
+// Timing-only builds (make stamps): per-workgroup s_memrealtime (100 MHz) stamps
+// [start, first tile visible, main loop done, end, hw_id | xcc_id << 32].
+__device__ unsigned long long g_stamps[5 * 65536];
+#define DP_STAMP(v)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");    \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  } while (0)
+#define DP_STAMPS_DECL unsigned long long st0_ = 0, st1_ = 0, st2_ = 0, st3_ = 0
+#define DP_STAMP_SAVE(wg)                                                             \
+  do {                                                                                \
+    if (threadIdx.x == 0 && (wg) < 65536) {                                           \
+      unsigned hw_, xcc_;                                                             \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));              \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));            \
+      unsigned long long* d_ = g_stamps + 5 * (wg);                                   \
+      d_[0] = st0_; d_[1] = st1_; d_[2] = st2_; d_[3] = st3_;                         \
+      d_[4] = hw_ | ((unsigned long long)xcc_ << 32);                                 \
+    }                                                                                 \
+  } while (0)
+#else
+#define DP_STAMP(v) do { } while (0)
+#define DP_STAMPS_DECL
+#define DP_STAMP_SAVE(wg) do { } while (0)
+#endif
+
 // 16 zero bytes x 8: source of the implicit-conv zero padding for LDS-DMA loads
 __device__ __attribute__((aligned(16))) uint32_t g_zero_page[32];
 
@@ -197,6 +225,123 @@ __device__ __forceinline__ void epilogue8(const GemmP& p, int m, int n, float (&
   }
 }
 
+// Row-staged epilogue for the big engines.  Per-column operands (bias, LayerScale
+// gamma) are loaded once per lane -- a lane keeps the same 8 columns for the whole
+// tile -- and each batch of NIT rows issues ALL of its row-dependent loads
+// (residuals, the fp32 C being accumulated into) before any arithmetic or store, so
+// their latencies overlap instead of serialising behind the stores.
+struct ColConst {
+  float b[8], g[8];
+};
+__device__ __forceinline__ void load_colconst(const GemmP& p, int n, ColConst& c) {
+  const bool ok = n < p.N;
+  if (p.bias && ok) {
+    const float4 x = *(const float4*)(p.bias + n), y = *(const float4*)(p.bias + n + 4);
+    c.b[0] = x.x; c.b[1] = x.y; c.b[2] = x.z; c.b[3] = x.w; c.b[4] = y.x; c.b[5] = y.y; c.b[6] = y.z; c.b[7] = y.w;
+  } else {
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) c.b[r] = 0.f;
+  }
+  if (p.gamma && ok) {
+    const float4 x = *(const float4*)(p.gamma + n), y = *(const float4*)(p.gamma + n + 4);
+    c.g[0] = x.x; c.g[1] = x.y; c.g[2] = x.z; c.g[3] = x.w; c.g[4] = y.x; c.g[5] = y.y; c.g[6] = y.z; c.g[7] = y.w;
+  } else {
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) c.g[r] = 1.f;
+  }
+}
+__device__ __forceinline__ long long out_offset(const GemmP& p, int m, int n) {
+  if (p.store_mode == DP_STORE_DECONV2X2) {
+    const int hw = p.dc_h * p.dc_w;
+    const int b = m / hw, rr = m - b * hw;
+    const int y = rr / p.dc_w, x = rr - y * p.dc_w;
+    const int q = n / p.dc_cout, co = n - q * p.dc_cout;
+    const long long pix = ((long long)b * 2 * p.dc_h + 2 * y + (q >> 1)) * (2 * p.dc_w) + 2 * x + (q & 1);
+    return pix * p.ldc + co;
+  }
+  long long row = m;
+  if (p.row_group) row = (long long)(m / p.row_group) * p.row_group_out + p.row_off + m % p.row_group;
+  return row * p.ldc + n;
+}
+template <typename K_>
+__device__ __forceinline__ void add8_u4(float (&v)[8], uint4 r) {
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  #pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] += K_::to_f(w[k] & 0xffff);
+    v[2 * k + 1] += K_::to_f(w[k] >> 16);
+  }
+}
+// v[it][0..7] = accumulators of row ms[it], columns n..n+7.
+template <typename K_, int NIT>
+__device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc, const int (&ms)[NIT], int n,
+                                              float (&v)[NIT][8]) {
+  const bool nok = n < p.N;
+  bool ok[NIT];
+  long long off[NIT];
+  #pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    ok[it] = nok && ms[it] < p.M;
+    off[it] = out_offset(p, ok[it] ? ms[it] : 0, n);
+  }
+  uint4 r1[NIT], r2[NIT];
+  float4 c0[NIT], c1[NIT];
+  const uint4 z4 = {0u, 0u, 0u, 0u};
+  const float4 zf = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.R1) {
+    #pragma unroll
+    for (int it = 0; it < NIT; ++it) r1[it] = ok[it] ? *(const uint4*)(p.R1 + (long long)ms[it] * p.ldr1 + n) : z4;
+  }
+  if (p.R2) {
+    #pragma unroll
+    for (int it = 0; it < NIT; ++it) r2[it] = ok[it] ? *(const uint4*)(p.R2 + (long long)ms[it] * p.ldr2 + n) : z4;
+  }
+  const bool acc32 = p.accumulate && p.c_dtype == DP_F32;
+  if (acc32) {
+    #pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const float* c = (const float*)p.C + off[it];
+      c0[it] = ok[it] ? *(const float4*)c : zf;
+      c1[it] = ok[it] ? *(const float4*)(c + 4) : zf;
+    }
+  }
+  #pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    float (&x)[8] = v[it];
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] += cc.b[r];
+    if (p.act == DP_ACT_RELU) {
+      #pragma unroll
+      for (int r = 0; r < 8; ++r) x[r] = fmaxf(x[r], 0.f);
+    } else if (p.act == DP_ACT_GELU) {
+      #pragma unroll
+      for (int r = 0; r < 8; ++r) x[r] = gelu_erf(x[r]);
+    }
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] *= cc.g[r];
+    if (p.pos && ok[it]) add8_f32(x, p.pos + (long long)(ms[it] % p.pos_group + p.pos_off) * p.ldpos + n);
+    if (p.R1) add8_u4<K_>(x, r1[it]);
+    if (p.R2) add8_u4<K_>(x, r2[it]);
+    if (!ok[it]) continue;
+    if (p.c_dtype == DP_F32) {
+      float* c = (float*)p.C + off[it];
+      if (acc32) {
+        x[0] += c0[it].x; x[1] += c0[it].y; x[2] += c0[it].z; x[3] += c0[it].w;
+        x[4] += c1[it].x; x[5] += c1[it].y; x[6] += c1[it].z; x[7] += c1[it].w;
+      }
+      *(float4*)c = make_float4(x[0], x[1], x[2], x[3]);
+      *(float4*)(c + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    } else {
+      uint4 o;
+      o.x = (uint32_t)K_::from_f(x[0]) | ((uint32_t)K_::from_f(x[1]) << 16);
+      o.y = (uint32_t)K_::from_f(x[2]) | ((uint32_t)K_::from_f(x[3]) << 16);
+      o.z = (uint32_t)K_::from_f(x[4]) | ((uint32_t)K_::from_f(x[5]) << 16);
+      o.w = (uint32_t)K_::from_f(x[6]) | ((uint32_t)K_::from_f(x[7]) << 16);
+      *(uint4*)((u16*)p.C + off[it]) = o;
+    }
+  }
+}
+
 // implicit-conv row descriptor: output pixel m -> top-left input tap
 struct ConvRow {
   int iy, ix, pix;
@@ -298,6 +443,8 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
+  DP_STAMPS_DECL;
+  DP_STAMP(st0_);
 
   // LDS-DMA piece i of this thread covers tile row i*ROWS_PER_ROUND + wave*ROWS_PER_WAVE_PIECE + lane/CR;
   // LDS slot lane%CR of that row holds logical chunk (lane%CR) ^ swz(row): the swizzle is
@@ -391,6 +538,9 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
     for (int kt = 0; kt < KT; ++kt) {
       wait_vmcnt<0>();
       lds_barrier();
+#ifdef DP_STAMPS
+      if (kt == 0) DP_STAMP(st1_);
+#endif
       if (kt + 1 < KT && !(p.dbg & 2)) issue(kt + 1, stage ^ 1);
       if (p.dbg & 4) {
         const u16* sa = (const u16*)(smem + stage * STAGE);
@@ -436,6 +586,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       if (t < KT) issue(t, t);
     wait_tile(0);
     lds_barrier();
+    DP_STAMP(st1_);
     rd(fa0, fb0, 0, 0);
     int stage = 0;
     if constexpr (KS == 2) {
@@ -486,6 +637,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
     }
   }
 
+  DP_STAMP(st2_);
   if (p.dbg & 1) {
     #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -504,8 +656,175 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   constexpr int CPR = TN / 8;                 // 8-column chunks per row
   constexpr int RPI = 64 / CPR;               // rows per read instruction
   float* stg = (float*)smem + wave * (32 * SROW);
+  constexpr int NIT = 32 / RPI;
+  const int c8 = (lane % CPR) * 8, n_l = n0 + wn * TN + c8;
+  ColConst cc;
+  load_colconst(p, n_l, cc);
   #pragma unroll
   for (int q = 0; q < FM / 2; ++q) {          // 32 rows (two 16-row fragments) per pass
+    #pragma unroll
+    for (int i = 0; i < 2; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j)
+        *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[2 * q + i][j];
+    float v[NIT][8];
+    int ms[NIT];
+    #pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int row = it * RPI + lane / CPR;
+      const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
+      const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
+      ms[it] = m0 + wm * TM + q * 32 + row;
+    }
+    epilogue_rows<K_, NIT>(p, cc, ms, n_l, v);
+  }
+  DP_STAMP(st3_);
+  DP_STAMP_SAVE(wgid);
+}
+
+// ======================================================= 4-wave 256x256 engine
+// 256 x 256 x 64 tile, 4 waves (2 x 2), wave tile 128 x 128: one wave per SIMD
+// with its 256 fp32 accumulators in AGPRs (512-entry unified register file),
+// so each 16x16x32 MFMA costs 0.25 LDS fragment reads (vs 0.375 for a 128 x 64
+// wave tile) and the LDS read stream keeps pace with the matrix pipe.  Both
+// k sub-steps' fragments are read up front (two register sets) so the second
+// set's LDS latency hides under the first 64 MFMAs.  2-stage LDS-DMA ring.
+#ifndef W4SB
+#define SB() __builtin_amdgcn_sched_barrier(0)
+#endif
+template <typename K_, bool CONV, bool RELU>
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmP p) {
+  constexpr int TILEB = 2 * 256 * 128;     // A + B, bytes per stage
+  constexpr int A_BYTES = 256 * 128;
+  constexpr int TM = 128, TN = 128, FM = 8, FN = 8;
+  constexpr int EPI_BYTES = 4 * 32 * (TN + 4) * 4;
+  constexpr int SMEM = 2 * TILEB > EPI_BYTES ? 2 * TILEB : EPI_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
+  const int m0 = tile_m * 256, n0 = tile_n * 256;
+
+  // LDS-DMA piece i (0..7) of this thread: tile row i*32 + wave*8 + lane/8
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  int a_row[8], b_row[8];
+  ConvRow a_cr[8];
+  #pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + i * 32 + prow, n = n0 + i * 32 + prow;
+    if constexpr (CONV) a_cr[i] = conv_row(p, m);
+    else a_row[i] = m < p.M ? m : p.M - 1;
+    b_row[i] = n < p.N ? n : p.N - 1;
+  }
+  int t_ky = 0, t_kx = 0, t_ci = 0;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
+  auto issue = [&](int kt, int stage) {
+    const uint32_t sa = lds_base + stage * TILEB, sb = sa + A_BYTES;
+    const int k0 = kt * 64;
+    #pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const void* src;
+      if constexpr (CONV) {
+        bool inb;
+        const u16* s = conv_src(p, a_cr[i], t_ky, t_kx, t_ci + pchunk * 8, inb);
+        src = inb ? (const void*)s : (const void*)g_zero_page;
+      } else {
+        src = p.A + (long long)a_row[i] * p.lda + k0 + pchunk * 8;
+      }
+      glds16(src, sa + i * 4096);
+    }
+    if constexpr (CONV) {
+      t_ci += 64;
+      if (t_ci == p.in_c) {
+        t_ci = 0;
+        if (++t_kx == p.k_w) { t_kx = 0; ++t_ky; }
+      }
+    }
+    #pragma unroll
+    for (int i = 0; i < 8; ++i) glds16(p.B + (long long)b_row[i] * p.ldb + k0 + pchunk * 8, sb + i * 4096);
+  };
+
+  f32x4_t acc[FM][FN];
+  #pragma unroll
+  for (int i = 0; i < FM; ++i)
+    #pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int frow = lane & 15, fchunk = lane >> 4;
+  // fragment g of a k sub-step: g < 8 -> B rows wn*128 + g*16, else A rows wm*128 + (g-8)*16
+  auto rd = [&](int stage, int ks, int g) -> uint4 {
+    const char* base = smem + stage * TILEB + (g < 8 ? A_BYTES : 0);
+    const int row = (g < 8 ? wn * TN + g * 16 : wm * TM + (g - 8) * 16) + frow;
+    return *(const uint4*)((const u16*)base + lds_off(row, ks * 4 + fchunk));
+  };
+  auto mma = [&](uint4 (&f)[16], int t) {
+    const int i = t >> 3, j = t & 7;
+    uint4 a = f[8 + i];
+    if constexpr (RELU) a = relu_pk16(a);
+    acc[i][j] = K_::mfma16(f[j], a, acc[i][j]);
+  };
+
+  // Software pipeline, one barrier per 64-deep k step; X = sub-step 0 fragments,
+  // Y = sub-step 1.  Iteration kt (tile kt in stage s, X already loaded):
+  //   A: read Y from s, interleaved 1:2 with X's first 32 MFMAs, then the rest
+  //   B: tile kt+1 landed (own vmcnt) + barrier (all landed; everyone done with s)
+  //      -> DMA tile kt+2 into s interleaved with Y MFMAs, then read X of tile
+  //      kt+1 from s^1 interleaved with the remaining Y MFMAs.
+  const int KT = p.K / 64;
+  uint4 X[16], Y[16];
+  issue(0, 0);
+  wait_vmcnt<0>();
+  lds_barrier();
+  if (KT > 1) issue(1, 1);
+  #pragma unroll
+  for (int g = 0; g < 16; ++g) X[g] = rd(0, 0, g);
+  int stage = 0;
+  for (int kt = 0; kt < KT; ++kt) {
+    #pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      Y[g] = rd(stage, 1, g);
+      mma(X, 2 * g);
+      mma(X, 2 * g + 1);
+      SB();
+    }
+    #pragma unroll
+    for (int t = 32; t < 64; ++t) mma(X, t);
+    SB();
+    if (kt + 1 < KT) {
+      wait_vmcnt<0>();
+      lds_barrier();
+      if (kt + 2 < KT) issue(kt + 2, stage);
+      SB();
+      #pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        X[g] = rd(stage ^ 1, 0, g);
+        mma(Y, 2 * g);
+        mma(Y, 2 * g + 1);
+        SB();
+      }
+      #pragma unroll
+      for (int t = 32; t < 64; ++t) mma(Y, t);
+    } else {
+      #pragma unroll
+      for (int t = 0; t < 64; ++t) mma(Y, t);
+    }
+    SB();
+    stage ^= 1;
+  }
+
+  lds_barrier();
+  constexpr int SROW = TN + 4, CPR = TN / 8, RPI = 64 / CPR;
+  float* stg = (float*)smem + wave * (32 * SROW);
+  #pragma unroll
+  for (int q = 0; q < FM / 2; ++q) {
     #pragma unroll
     for (int i = 0; i < 2; ++i)
       #pragma unroll
@@ -521,6 +840,203 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       if (m < p.M && n < p.N) epilogue8<K_>(p, m, n, v);
     }
   }
+}
+
+template <typename K_>
+int launch_w4(const GemmP& p0, bool conv, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = (p.N + 255) / 256;
+  dim3 grid(p.tiles_n * ((p.M + 255) / 256));
+  if (conv && p.relu_a) hipLaunchKernelGGL((gemm_w4_kernel<K_, true, true>), grid, dim3(256), 0, s, p);
+  else if (conv) hipLaunchKernelGGL((gemm_w4_kernel<K_, true, false>), grid, dim3(256), 0, s, p);
+  else if (p.relu_a) hipLaunchKernelGGL((gemm_w4_kernel<K_, false, true>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gemm_w4_kernel<K_, false, false>), grid, dim3(256), 0, s, p);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+// ======================================================= 8-phase 256x256 engine
+// 256 x 256 x 64 tile, 8 waves (2 x 4, wave tile 128 x 64), K loop cut into 4
+// phases per K tile -- one 64 x 32 C quadrant x K 64 = 16 MFMAs per wave per
+// phase -- each phase {fragment ds_reads, ONE half-tile LDS-DMA prefetch,
+// s_barrier, lgkmcnt(0), 16 MFMAs at raised priority, s_barrier}.  The LDS
+// holds 2 K tiles as 4 half-tiles each (A rows 0-127 / 128-255, B cols
+// 0-127 / 128-255, 16 KiB each); a half is refilled one phase after its last
+// read, so global loads stream continuously with up to 3 half-tiles in flight
+// and the only vmcnt wait is once per K tile (counted, never a drain while
+// tiles remain).  Quadrant order (qm,qn): (0,0) (0,1) (1,0) (1,1); reads:
+// p0 A(qm0)+B(qn0), p1 B(qn1), p2 A(qm1), p3 none.  Issue order of tile
+// t+1 / t+2 halves: p0 A0(t+1), p1 A1(t+1), p2 B0(t+2), p3 B1(t+2).
+template <typename K_, bool CONV, bool RELU>
+__global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
+  constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
+  constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
+  constexpr int TN = 64, TM = 128;
+  constexpr int EPI_BYTES = 8 * 32 * (TN + 4) * 4;
+  constexpr int SMEM = 2 * TILEB > EPI_BYTES ? 2 * TILEB : EPI_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
+  const int m0 = tile_m * 256, n0 = tile_n * 256;
+
+  // LDS-DMA pieces: half-tile row r = i*64 + wave*8 + lane/8 (i = 0,1), swizzle on the source
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  const u16* a_src[2][2];
+  ConvRow a_cr[2][2];
+  const u16* b_src[2][2];
+  #pragma unroll
+  for (int h = 0; h < 2; ++h)
+    #pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + 128 * h + i * 64 + prow;
+      if constexpr (CONV) a_cr[h][i] = conv_row(p, m);
+      else a_src[h][i] = p.A + (long long)(m < p.M ? m : p.M - 1) * p.lda + pchunk * 8;
+      const int n = n0 + 128 * h + i * 64 + prow;
+      b_src[h][i] = p.B + (long long)(n < p.N ? n : p.N - 1) * p.ldb + pchunk * 8;
+    }
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
+  auto issueA = [&](int h, int t) {  // A half h of K tile t -> buffer t&1
+    const uint32_t dst = lds_base + (t & 1) * TILEB + h * HALF;
+    int ci = 0, ky = 0, kx = 0;
+    if constexpr (CONV) {
+      const int k0 = t * 64, tap = k0 / p.in_c;
+      ci = k0 - tap * p.in_c;
+      ky = tap / p.k_w;
+      kx = tap - ky * p.k_w;
+    }
+    #pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const void* src;
+      if constexpr (CONV) {
+        bool inb;
+        const u16* s = conv_src(p, a_cr[h][i], ky, kx, ci + pchunk * 8, inb);
+        src = inb ? (const void*)s : (const void*)g_zero_page;
+      } else {
+        src = a_src[h][i] + t * 64;
+      }
+      glds16(src, dst + i * 8192);
+    }
+  };
+  auto issueB = [&](int h, int t) {
+    const uint32_t dst = lds_base + (t & 1) * TILEB + (2 + h) * HALF;
+    #pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(b_src[h][i] + t * 64, dst + i * 8192);
+  };
+
+  f32x4_t acc[8][4];
+  #pragma unroll
+  for (int i = 0; i < 8; ++i)
+    #pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int frow = lane & 15, fchunk = lane >> 4;
+  uint4 af[2][4], bf[2][2][2];
+  auto readA = [&](int qm, int buf) {
+    const u16* sa = (const u16*)(smem + buf * TILEB + wm * HALF);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+        af[ks][fm] = *(const uint4*)(sa + lds_off(qm * 64 + fm * 16 + frow, ks * 4 + fchunk));
+  };
+  auto readB = [&](int qn, int buf) {
+    const u16* sb = (const u16*)(smem + buf * TILEB + (2 + (wn >> 1)) * HALF);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+        bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((wn & 1) * 64 + qn * 32 + fn * 16 + frow, ks * 4 + fchunk));
+  };
+  auto mma = [&](int qm, int qn) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fm = 0; fm < 4; ++fm) {
+        uint4 a = af[ks][fm];
+        if constexpr (RELU) a = relu_pk16(a);
+        #pragma unroll
+        for (int fn = 0; fn < 2; ++fn)
+          acc[qm * 4 + fm][qn * 2 + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * 2 + fn]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
+
+  const int KT = p.K / 64;
+  issueA(0, 0); issueA(1, 0); issueB(0, 0); issueB(1, 0);
+  if (KT > 1) {
+    issueB(0, 1); issueB(1, 1);
+    wait_vmcnt<4>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  lds_barrier();
+  for (int t = 0; t < KT; ++t) {
+    const int buf = t & 1;
+    const bool n1 = t + 1 < KT, n2 = t + 2 < KT;
+    // phase 0: quadrant (0,0)
+    readA(0, buf); readB(0, buf);
+    if (n1) issueA(0, t + 1);
+    bar(); mma(0, 0); bar();
+    // phase 1: quadrant (0,1)
+    readB(1, buf);
+    if (n1) issueA(1, t + 1);
+    bar(); mma(0, 1); bar();
+    // phase 2: quadrant (1,0)
+    readA(1, buf);
+    if (n2) issueB(0, t + 2);
+    bar(); mma(1, 0); bar();
+    // phase 3: quadrant (1,1); then tile t+1 must have landed
+    if (n2) issueB(1, t + 2);
+    bar(); mma(1, 1);
+    if (n2) wait_vmcnt<4>(); else wait_vmcnt<0>();
+    bar();
+  }
+
+  // epilogue: identical to the big engine (LDS-staged, row-coalesced)
+  lds_barrier();
+  constexpr int SROW = TN + 4, CPR = TN / 8, RPI = 64 / CPR;
+  float* stg = (float*)smem + wave * (32 * SROW);
+  #pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    #pragma unroll
+    for (int i = 0; i < 2; ++i)
+      #pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[2 * q + i][j];
+    #pragma unroll
+    for (int r0 = 0; r0 < 32; r0 += RPI) {
+      const int row = r0 + lane / CPR, c8 = (lane % CPR) * 8;
+      const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
+      const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const int m = m0 + wm * TM + q * 32 + row, n = n0 + wn * TN + c8;
+      if (m < p.M && n < p.N) epilogue8<K_>(p, m, n, v);
+    }
+  }
+}
+
+template <typename K_>
+int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = (p.N + 255) / 256;
+  dim3 grid(p.tiles_n * ((p.M + 255) / 256));
+  if (conv && p.relu_a) hipLaunchKernelGGL((gemm_8ph_kernel<K_, true, true>), grid, dim3(512), 0, s, p);
+  else if (conv) hipLaunchKernelGGL((gemm_8ph_kernel<K_, true, false>), grid, dim3(512), 0, s, p);
+  else if (p.relu_a) hipLaunchKernelGGL((gemm_8ph_kernel<K_, false, true>), grid, dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((gemm_8ph_kernel<K_, false, false>), grid, dim3(512), 0, s, p);
+  DP_CHECK_LAUNCH();
+  return 0;
 }
 
 // ========================================================== small-tile engine
@@ -710,11 +1226,19 @@ int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
     case DP_TILE_BIG_256x128: return launch_big<K_, 128, 64>(p, conv, s);
     case DP_TILE_BIG_256x128_K32: return launch_big<K_, 128, 32>(p, conv, s);
     case DP_TILE_BIG_256x256_K32: return launch_big<K_, 256, 32>(p, conv, s);
+    case DP_TILE_8PH_256x256: return launch_8ph<K_>(p, conv, s);
+    case DP_TILE_W4_256x256: return launch_w4<K_>(p, conv, s);
     default: return launch_big<K_, 256, 64>(p, conv, s);
   }
 }
 
 }  // namespace
+
+#ifdef DP_STAMPS
+extern "C" int dp_gemm_stamps(void* host_dst, int n_wg) {
+  return (int)hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_stamps), (size_t)n_wg * 5 * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // Not part of the ABI header: ablation switches for the GEMM microbenchmark only.
 extern "C" int dp_gemm_debug_flags(int flags) {

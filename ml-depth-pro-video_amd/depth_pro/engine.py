@@ -17,6 +17,7 @@ f16), the ViT residual streams fp32.
 
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -24,6 +25,10 @@ import torch
 from . import ops
 from ._lib import DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DPError, load
 from .spec import DEPTH, EMBED_DIM, HEADS, IMG_SIZE, MLP_DIM, TOKENS
+
+# Timing ablations for tools/frame_ablation.py only (results are wrong when set):
+# comma list of {side, attn, ln, vitgemm, decoder, head}.
+_ABLATE = set(filter(None, os.environ.get("DP_ABLATE", "").split(",")))
 
 NWIN = 35
 TOK = TOKENS            # 577
@@ -216,16 +221,22 @@ class Engine:
         ops.vit_cls_rows(buf.x, P[pre + "cls"], P[pre + "pos"], n_img)
         for i in range(DEPTH):
             b = f"{pre}blocks.{i}."
-            ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
-            ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"])
-            ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS)
-            ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
-                     gamma=P[b + "ls1.gamma"], accumulate=True)
-            ops.layernorm(buf.x, P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, M, D)
-            ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
-                     act=DP_ACT_GELU)
-            ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
-                     gamma=P[b + "ls2.gamma"], accumulate=True)
+            if "ln" not in _ABLATE:
+                ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
+            if "vitgemm" not in _ABLATE:
+                ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"])
+            if "attn" not in _ABLATE:
+                ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS)
+            if "vitgemm" not in _ABLATE:
+                ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
+                         gamma=P[b + "ls1.gamma"], accumulate=True)
+            if "ln" not in _ABLATE:
+                ops.layernorm(buf.x, P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, M, D)
+            if "vitgemm" not in _ABLATE:
+                ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
+                         act=DP_ACT_GELU)
+                ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
+                         gamma=P[b + "ls2.gamma"], accumulate=True)
             if hooks and i in hooks:
                 hooks[i]()
         ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.h, M, D)
@@ -293,7 +304,8 @@ class Engine:
         ops.patchify_pyramid(self.x0, self.cols)
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
-            self._side_encoders()
+            if "side" not in _ABLATE:
+                self._side_encoders()
         vp = self.vp
         hooks = {
             5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
@@ -328,12 +340,17 @@ class Engine:
             self._conv3(self.fx, 24, 128, P["fov.h0.w"], self.f12, 64, bias=P["fov.h0.b"], act=DP_ACT_RELU, stride=2)
             self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
             ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
-        f = self._fusion(4, self.low, 48, None)
-        for i, (enc, s, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)), (1, (self.enc1, 384, 256))):
-            c = self.dec[s]["c"]
-            self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
-            f = self._fusion(i, f, s, c)
-        feats = self._fusion(0, f, 768, self.enc0)
+        if "decoder" not in _ABLATE:
+            f = self._fusion(4, self.low, 48, None)
+            for i, (enc, s, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)), (1, (self.enc1, 384, 256))):
+                c = self.dec[s]["c"]
+                self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
+                f = self._fusion(i, f, s, c)
+            feats = self._fusion(0, f, 768, self.enc0)
+        else:
+            feats = self.feats
+        if "head" in _ABLATE:
+            return self.canonical, self.fov_deg
         # head (depth_pro.py:182-207): conv3x3 -> deconv -> conv3x3+ReLU -> 1x1+ReLU (fused)
         self._conv3(feats, 768, 256, P["head.0.w"], self.h0, 128, bias=P["head.0.b"])
         self._deconv(self.h0, 768, 128, P["head.1.w"], self.h1, 128, bias=P["head.1.b"])

@@ -227,3 +227,30 @@ def test_normalize_u8(cuda):
     ops.normalize_u8(torch.from_numpy(img).to(cuda), out)
     ref = (torch.from_numpy(img).permute(2, 0, 1).float().div(255) - 0.5) / 0.5
     assert torch.equal(out.cpu(), ref)
+
+
+TILES = {"128x128": 1, "256x64": 2, "256x32": 3, "big256x256": 4, "big256x128": 5, "big256x256k32": 6,
+         "big256x128k32": 7, "8ph256x256": 8, "w4_256x256": 9}
+
+
+@pytest.mark.parametrize("tile", list(TILES))
+def test_gemm_every_tile_engine(cuda, tile):
+    """Every tile engine, dense (ragged M) and implicit-conv with ReLU prologue, vs fp32 torch."""
+    dt = torch.bfloat16
+    g = torch.Generator().manual_seed(TILES[tile])
+    M, N, K = 1000, 256, 1024
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    C = torch.empty(M, N, dtype=dt, device=cuda)
+    ops.gemm(A, B, C, M=M, N=N, K=K, bias=bias, tile=TILES[tile])
+    close(C, A.float() @ B.float().t() + bias, dt, f"dense {tile}")
+    S, cin, cout = 40, 128, 256
+    x = rnd(1, cin, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(cout, cin, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * cin) ** -0.5)
+    out = torch.empty(S * S, cout, dtype=dt, device=cuda)
+    ops.gemm(x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous(), out,
+             M=S * S, N=cout, K=9 * cin, conv=dict(in_h=S, in_w=S, in_c=cin, k=3, stride=1, pad=1, out_h=S, out_w=S),
+             relu_a=True, tile=TILES[tile])
+    ref = F.conv2d(F.relu(x.float()), w.float(), padding=1)
+    close(out.reshape(1, S, S, cout).permute(0, 3, 1, 2), ref, dt, f"conv {tile}")
