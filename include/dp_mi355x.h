@@ -103,7 +103,7 @@ typedef struct dp_gemm_args {
 
 enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32 = 3,
        DP_TILE_BIG_256x256 = 4, DP_TILE_BIG_256x128 = 5, DP_TILE_BIG_256x256_K32 = 6,
-       DP_TILE_BIG_256x128_K32 = 7, DP_TILE_8PH_256x256 = 8, DP_TILE_W4_256x256 = 9 };
+       DP_TILE_BIG_256x128_K32 = 7, DP_TILE_8PH_256x256 = 8 };
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 

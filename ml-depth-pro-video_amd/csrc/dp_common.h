@@ -11,6 +11,9 @@ typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(16))) float f32x16_t;
 typedef __attribute__((ext_vector_type(2))) short i16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
 
 // 16-bit element kinds.  Activations and weights are carried as raw u16 bits;
 // the kind only decides the MFMA opcode and the float<->16-bit conversions.
@@ -21,6 +24,10 @@ struct KBF16 {
   }
   static __device__ __forceinline__ u16 from_f(float f) {
     return __builtin_bit_cast(u16, (__bf16)f);
+  }
+  // two floats -> packed pair (a in the low half), one v_cvt_pk_bf16_f32 (RNE)
+  static __device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
   }
   static __device__ __forceinline__ f32x4_t mfma16(uint4 a, uint4 b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
@@ -39,6 +46,9 @@ struct KF16 {
   }
   static __device__ __forceinline__ u16 from_f(float f) {
     return __builtin_bit_cast(u16, (_Float16)f);
+  }
+  static __device__ __forceinline__ uint32_t pack2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, f16x2_t));
   }
   static __device__ __forceinline__ f32x4_t mfma16(uint4 a, uint4 b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a),

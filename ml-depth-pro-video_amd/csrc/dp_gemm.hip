@@ -272,37 +272,38 @@ __device__ __forceinline__ void add8_u4(float (&v)[8], uint4 r) {
     v[2 * k + 1] += K_::to_f(w[k] >> 16);
   }
 }
-// v[it][0..7] = accumulators of row ms[it], columns n..n+7.
+// v[it][0..7] = accumulators of row ms[it], columns n..n+7.  Loads go to clamped
+// (always valid) rows with no predicate, so the compiler issues the whole batch
+// back to back instead of sinking each load into its own branch; only the
+// stores are predicated.
 template <typename K_, int NIT>
 __device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc, const int (&ms)[NIT], int n,
                                               float (&v)[NIT][8]) {
-  const bool nok = n < p.N;
-  bool ok[NIT];
+  const int nc = n < p.N ? n : p.N - 8;
+  int mc[NIT];
   long long off[NIT];
   #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    ok[it] = nok && ms[it] < p.M;
-    off[it] = out_offset(p, ok[it] ? ms[it] : 0, n);
+    mc[it] = ms[it] < p.M ? ms[it] : p.M - 1;
+    off[it] = out_offset(p, mc[it], nc);
   }
   uint4 r1[NIT], r2[NIT];
   float4 c0[NIT], c1[NIT];
-  const uint4 z4 = {0u, 0u, 0u, 0u};
-  const float4 zf = make_float4(0.f, 0.f, 0.f, 0.f);
   if (p.R1) {
     #pragma unroll
-    for (int it = 0; it < NIT; ++it) r1[it] = ok[it] ? *(const uint4*)(p.R1 + (long long)ms[it] * p.ldr1 + n) : z4;
+    for (int it = 0; it < NIT; ++it) r1[it] = *(const uint4*)(p.R1 + (long long)mc[it] * p.ldr1 + nc);
   }
   if (p.R2) {
     #pragma unroll
-    for (int it = 0; it < NIT; ++it) r2[it] = ok[it] ? *(const uint4*)(p.R2 + (long long)ms[it] * p.ldr2 + n) : z4;
+    for (int it = 0; it < NIT; ++it) r2[it] = *(const uint4*)(p.R2 + (long long)mc[it] * p.ldr2 + nc);
   }
   const bool acc32 = p.accumulate && p.c_dtype == DP_F32;
   if (acc32) {
     #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const float* c = (const float*)p.C + off[it];
-      c0[it] = ok[it] ? *(const float4*)c : zf;
-      c1[it] = ok[it] ? *(const float4*)(c + 4) : zf;
+      c0[it] = *(const float4*)c;
+      c1[it] = *(const float4*)(c + 4);
     }
   }
   #pragma unroll
@@ -319,16 +320,21 @@ __device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc
     }
     #pragma unroll
     for (int r = 0; r < 8; ++r) x[r] *= cc.g[r];
-    if (p.pos && ok[it]) add8_f32(x, p.pos + (long long)(ms[it] % p.pos_group + p.pos_off) * p.ldpos + n);
+    if (p.pos) add8_f32(x, p.pos + (long long)(mc[it] % p.pos_group + p.pos_off) * p.ldpos + nc);
     if (p.R1) add8_u4<K_>(x, r1[it]);
     if (p.R2) add8_u4<K_>(x, r2[it]);
-    if (!ok[it]) continue;
+    if (acc32) {
+      x[0] += c0[it].x; x[1] += c0[it].y; x[2] += c0[it].z; x[3] += c0[it].w;
+      x[4] += c1[it].x; x[5] += c1[it].y; x[6] += c1[it].z; x[7] += c1[it].w;
+    }
+  }
+  const bool nok = n < p.N;
+  #pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const float (&x)[8] = v[it];
+    if (!(nok && ms[it] < p.M)) continue;
     if (p.c_dtype == DP_F32) {
       float* c = (float*)p.C + off[it];
-      if (acc32) {
-        x[0] += c0[it].x; x[1] += c0[it].y; x[2] += c0[it].z; x[3] += c0[it].w;
-        x[4] += c1[it].x; x[5] += c1[it].y; x[6] += c1[it].z; x[7] += c1[it].w;
-      }
       *(float4*)c = make_float4(x[0], x[1], x[2], x[3]);
       *(float4*)(c + 4) = make_float4(x[4], x[5], x[6], x[7]);
     } else {
@@ -682,177 +688,6 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   }
   DP_STAMP(st3_);
   DP_STAMP_SAVE(wgid);
-}
-
-// ======================================================= 4-wave 256x256 engine
-// 256 x 256 x 64 tile, 4 waves (2 x 2), wave tile 128 x 128: one wave per SIMD
-// with its 256 fp32 accumulators in AGPRs (512-entry unified register file),
-// so each 16x16x32 MFMA costs 0.25 LDS fragment reads (vs 0.375 for a 128 x 64
-// wave tile) and the LDS read stream keeps pace with the matrix pipe.  Both
-// k sub-steps' fragments are read up front (two register sets) so the second
-// set's LDS latency hides under the first 64 MFMAs.  2-stage LDS-DMA ring.
-#ifndef W4SB
-#define SB() __builtin_amdgcn_sched_barrier(0)
-#endif
-template <typename K_, bool CONV, bool RELU>
-__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const GemmP p) {
-  constexpr int TILEB = 2 * 256 * 128;     // A + B, bytes per stage
-  constexpr int A_BYTES = 256 * 128;
-  constexpr int TM = 128, TN = 128, FM = 8, FN = 8;
-  constexpr int EPI_BYTES = 4 * 32 * (TN + 4) * 4;
-  constexpr int SMEM = 2 * TILEB > EPI_BYTES ? 2 * TILEB : EPI_BYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
-  const int m0 = tile_m * 256, n0 = tile_n * 256;
-
-  // LDS-DMA piece i (0..7) of this thread: tile row i*32 + wave*8 + lane/8
-  const int prow = wave * 8 + (lane >> 3);
-  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
-  int a_row[8], b_row[8];
-  ConvRow a_cr[8];
-  #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + i * 32 + prow, n = n0 + i * 32 + prow;
-    if constexpr (CONV) a_cr[i] = conv_row(p, m);
-    else a_row[i] = m < p.M ? m : p.M - 1;
-    b_row[i] = n < p.N ? n : p.N - 1;
-  }
-  int t_ky = 0, t_kx = 0, t_ci = 0;
-  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
-  auto issue = [&](int kt, int stage) {
-    const uint32_t sa = lds_base + stage * TILEB, sb = sa + A_BYTES;
-    const int k0 = kt * 64;
-    #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const void* src;
-      if constexpr (CONV) {
-        bool inb;
-        const u16* s = conv_src(p, a_cr[i], t_ky, t_kx, t_ci + pchunk * 8, inb);
-        src = inb ? (const void*)s : (const void*)g_zero_page;
-      } else {
-        src = p.A + (long long)a_row[i] * p.lda + k0 + pchunk * 8;
-      }
-      glds16(src, sa + i * 4096);
-    }
-    if constexpr (CONV) {
-      t_ci += 64;
-      if (t_ci == p.in_c) {
-        t_ci = 0;
-        if (++t_kx == p.k_w) { t_kx = 0; ++t_ky; }
-      }
-    }
-    #pragma unroll
-    for (int i = 0; i < 8; ++i) glds16(p.B + (long long)b_row[i] * p.ldb + k0 + pchunk * 8, sb + i * 4096);
-  };
-
-  f32x4_t acc[FM][FN];
-  #pragma unroll
-  for (int i = 0; i < FM; ++i)
-    #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int frow = lane & 15, fchunk = lane >> 4;
-  // fragment g of a k sub-step: g < 8 -> B rows wn*128 + g*16, else A rows wm*128 + (g-8)*16
-  auto rd = [&](int stage, int ks, int g) -> uint4 {
-    const char* base = smem + stage * TILEB + (g < 8 ? A_BYTES : 0);
-    const int row = (g < 8 ? wn * TN + g * 16 : wm * TM + (g - 8) * 16) + frow;
-    return *(const uint4*)((const u16*)base + lds_off(row, ks * 4 + fchunk));
-  };
-  auto mma = [&](uint4 (&f)[16], int t) {
-    const int i = t >> 3, j = t & 7;
-    uint4 a = f[8 + i];
-    if constexpr (RELU) a = relu_pk16(a);
-    acc[i][j] = K_::mfma16(f[j], a, acc[i][j]);
-  };
-
-  // Software pipeline, one barrier per 64-deep k step; X = sub-step 0 fragments,
-  // Y = sub-step 1.  Iteration kt (tile kt in stage s, X already loaded):
-  //   A: read Y from s, interleaved 1:2 with X's first 32 MFMAs, then the rest
-  //   B: tile kt+1 landed (own vmcnt) + barrier (all landed; everyone done with s)
-  //      -> DMA tile kt+2 into s interleaved with Y MFMAs, then read X of tile
-  //      kt+1 from s^1 interleaved with the remaining Y MFMAs.
-  const int KT = p.K / 64;
-  uint4 X[16], Y[16];
-  issue(0, 0);
-  wait_vmcnt<0>();
-  lds_barrier();
-  if (KT > 1) issue(1, 1);
-  #pragma unroll
-  for (int g = 0; g < 16; ++g) X[g] = rd(0, 0, g);
-  int stage = 0;
-  for (int kt = 0; kt < KT; ++kt) {
-    #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      Y[g] = rd(stage, 1, g);
-      mma(X, 2 * g);
-      mma(X, 2 * g + 1);
-      SB();
-    }
-    #pragma unroll
-    for (int t = 32; t < 64; ++t) mma(X, t);
-    SB();
-    if (kt + 1 < KT) {
-      wait_vmcnt<0>();
-      lds_barrier();
-      if (kt + 2 < KT) issue(kt + 2, stage);
-      SB();
-      #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        X[g] = rd(stage ^ 1, 0, g);
-        mma(Y, 2 * g);
-        mma(Y, 2 * g + 1);
-        SB();
-      }
-      #pragma unroll
-      for (int t = 32; t < 64; ++t) mma(Y, t);
-    } else {
-      #pragma unroll
-      for (int t = 0; t < 64; ++t) mma(Y, t);
-    }
-    SB();
-    stage ^= 1;
-  }
-
-  lds_barrier();
-  constexpr int SROW = TN + 4, CPR = TN / 8, RPI = 64 / CPR;
-  float* stg = (float*)smem + wave * (32 * SROW);
-  #pragma unroll
-  for (int q = 0; q < FM / 2; ++q) {
-    #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[2 * q + i][j];
-    #pragma unroll
-    for (int r0 = 0; r0 < 32; r0 += RPI) {
-      const int row = r0 + lane / CPR, c8 = (lane % CPR) * 8;
-      const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
-      const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const int m = m0 + wm * TM + q * 32 + row, n = n0 + wn * TN + c8;
-      if (m < p.M && n < p.N) epilogue8<K_>(p, m, n, v);
-    }
-  }
-}
-
-template <typename K_>
-int launch_w4(const GemmP& p0, bool conv, hipStream_t s) {
-  GemmP p = p0;
-  p.tiles_n = (p.N + 255) / 256;
-  dim3 grid(p.tiles_n * ((p.M + 255) / 256));
-  if (conv && p.relu_a) hipLaunchKernelGGL((gemm_w4_kernel<K_, true, true>), grid, dim3(256), 0, s, p);
-  else if (conv) hipLaunchKernelGGL((gemm_w4_kernel<K_, true, false>), grid, dim3(256), 0, s, p);
-  else if (p.relu_a) hipLaunchKernelGGL((gemm_w4_kernel<K_, false, true>), grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((gemm_w4_kernel<K_, false, false>), grid, dim3(256), 0, s, p);
-  DP_CHECK_LAUNCH();
-  return 0;
 }
 
 // ======================================================= 8-phase 256x256 engine
@@ -1227,7 +1062,6 @@ int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
     case DP_TILE_BIG_256x128_K32: return launch_big<K_, 128, 32>(p, conv, s);
     case DP_TILE_BIG_256x256_K32: return launch_big<K_, 256, 32>(p, conv, s);
     case DP_TILE_8PH_256x256: return launch_8ph<K_>(p, conv, s);
-    case DP_TILE_W4_256x256: return launch_w4<K_>(p, conv, s);
     default: return launch_big<K_, 256, 64>(p, conv, s);
   }
 }

@@ -18,7 +18,7 @@ DP_ACT_NONE, DP_ACT_RELU, DP_ACT_GELU = 0, 1, 2
 DP_A_DENSE, DP_A_CONV = 0, 1
 DP_STORE_ROWS, DP_STORE_DECONV2X2 = 0, 1
 (DP_TILE_AUTO, DP_TILE_128x128, DP_TILE_256x64, DP_TILE_256x32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x128,
- DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256, DP_TILE_W4_256x256) = range(10)
+ DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256) = range(9)
 DP_ABI_VERSION = 1
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}

@@ -230,7 +230,7 @@ def test_normalize_u8(cuda):
 
 
 TILES = {"128x128": 1, "256x64": 2, "256x32": 3, "big256x256": 4, "big256x128": 5, "big256x256k32": 6,
-         "big256x128k32": 7, "8ph256x256": 8, "w4_256x256": 9}
+         "big256x128k32": 7, "8ph256x256": 8}
 
 
 @pytest.mark.parametrize("tile", list(TILES))

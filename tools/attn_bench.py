@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Time dp_attention on the Depth Pro ViT shapes vs torch SDPA on the same data."""
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
+from depth_pro import ops  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="only the 35 x 577 bf16 case, no torch reference")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    H, hd = 16, 64
+    cases = ((35, 577),) if args.quick else ((35, 577), (1, 577), (8, 2048))
+    for batch, seq in cases:
+        for dt in ((torch.bfloat16,) if args.quick else (torch.bfloat16, torch.float16)):
+            qkv = torch.randn(batch * seq, 3 * H * hd, device=dev).to(dt)
+            out = torch.empty(batch * seq, H * hd, dtype=dt, device=dev)
+            flop = 4.0 * batch * H * seq * seq * hd
+            ms = timeit(lambda: ops.attention(qkv, out, batch, seq, H, hd))
+            if args.quick:
+                print(f"b={batch} seq={seq} dp {ms*1e3:.1f}us {flop/ms/1e9:.1f}TF", flush=True)
+                continue
+            q, k, v = qkv.reshape(batch, seq, 3, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
+            ref = F.scaled_dot_product_attention(q.float(), k.float(), v.float()).transpose(1, 2).reshape(batch * seq, -1)
+            err = (out.float() - ref).abs().max().item()
+            qc, kc, vc = q.contiguous(), k.contiguous(), v.contiguous()
+            ms_t = timeit(lambda: F.scaled_dot_product_attention(qc, kc, vc))
+            print(f"b={batch:3d} seq={seq} {str(dt):15s} dp {ms*1e3:7.1f}us {flop/ms/1e9:6.1f}TF  max|err|={err:.2e}"
+                  f" | torch sdpa {ms_t*1e3:7.1f}us {flop/ms_t/1e9:6.1f}TF", flush=True)
+
+
+if __name__ == "__main__":
+    main()

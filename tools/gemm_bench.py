@@ -7,7 +7,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
 from depth_pro import ops  # noqa: E402
-from depth_pro._lib import (DP_TILE_128x128, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128, DP_TILE_W4_256x256,  # noqa
+from depth_pro._lib import (DP_TILE_128x128, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa
                             DP_TILE_BIG_256x128_K32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32)
 
 SHAPES = [  # (name, M, N, K, kw)
@@ -63,9 +63,8 @@ def main():
         flop = 2.0 * M * N * K
         res = []
         for tname, tile in (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
-                            ("8ph256x256", DP_TILE_8PH_256x256), ("w4_256x256", DP_TILE_W4_256x256)):
-            if tile in (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256,
-                        DP_TILE_W4_256x256) and N % 256:
+                            ("8ph256x256", DP_TILE_8PH_256x256)):
+            if tile in (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256) and N % 256:
                 continue
             if args.tile and args.tile != tname:
                 continue
@@ -87,8 +86,8 @@ def main():
             ops.gemm(A, B, C1, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_128x128)
             C2 = torch.empty_like(C)
             d = 0.0
-            for t in (DP_TILE_BIG_256x128, DP_TILE_8PH_256x256, DP_TILE_W4_256x256):
-                if t in (DP_TILE_8PH_256x256, DP_TILE_W4_256x256) and N % 256:
+            for t in (DP_TILE_BIG_256x128, DP_TILE_8PH_256x256):
+                if t == DP_TILE_8PH_256x256 and N % 256:
                     continue
                 ops.gemm(A, B, C2, M=M, N=N, K=K, conv=conv, bias=bias, tile=t)
                 d = max(d, (C1.float() - C2.float()).abs().max().item())
