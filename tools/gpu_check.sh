@@ -1,0 +1,35 @@
+#!/bin/bash
+# One bounded GPU session (run on the gpurun box from the repo root):
+#   GPU tests -> bench line -> rocprofv3 kernel-trace stats -> FETCH/WRITE PMC passes.
+# Every GPU step has its own time limit; the first failure ends the script.
+# Usage: tools/gpu_check.sh <tag> [tests|bench|prof|pmc ...]   (default: all four)
+set -eo pipefail
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-tests bench prof pmc}
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+for S in $STEPS; do
+  case $S in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > $OUT/pytest_gpu.log 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.log 2>&1 ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv \
+        -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1 ;;
+    pmc)
+      # separate passes (FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2); eager forward so every dispatch is attributed
+      timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc \
+        -- python3 tools/frame_once.py > $OUT/pmc_fetch.log 2>&1
+      timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc \
+        -- python3 tools/frame_once.py > $OUT/pmc_write.log 2>&1 ;;
+    *) echo "unknown step $S"; exit 2 ;;
+  esac
+  echo "step $S ok"
+done
