@@ -31,6 +31,30 @@ PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16/f16 MFMA (MI355X_MICROARCH.m
 PEAK_HBM_GBS = 8000.0
 
 
+TILE_NAMES = {1: "128x128", 2: "256x64", 3: "256x32", 4: "256x256", 5: "256x128", 8: "8phase-256x256",
+              12: "streamK-256x256", 13: "320x256"}
+TILE_KERNEL = {1: "gemm_kernel<KBF16, 128, 128", 4: "gemm_big_kernel<KBF16, 256, 256", 5: "gemm_big_kernel<KBF16, 256, 128",
+               8: "gemm_8ph_kernel<KBF16", 12: "gemm_sk_kernel<KBF16", 13: "gemm_big_kernel<KBF16, 320, 256"}
+
+
+def pmc_traffic(kernel: str, workgroups: int):
+    """HBM bytes per launch of `kernel` at `workgroups` from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json: tools/pmc_traffic.py over separate FETCH_SIZE / WRITE_SIZE passes,
+    FETCH_SIZE doubled per the gfx950 correction)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
+    for path in reversed(files):
+        try:
+            data = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for k in data.get("kernels", []):
+            if k["workgroups"] == workgroups and k["kernel"].startswith(kernel):
+                return {"bytes_per_launch": round(k["read_bytes_per_launch"] + k["write_bytes_per_launch"]),
+                        "source": os.path.relpath(path, REPO)}
+    return None
+
+
 def frame(seed: int) -> np.ndarray:
     return np.random.default_rng(seed=seed).integers(0, 256, (1536, 1536, 3), dtype=np.uint8)
 
@@ -132,25 +156,52 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     fps_per_gpu = fps / world
 
-    # per-kernel roofline leg: one instrumented eager frame, HIP events around every launch
-    kern = {}
+    # per-kernel roofline leg: one instrumented eager frame (side encoders serialised onto
+    # the main stream so no launch overlaps another), HIP events on the launching stream
+    # around every launch; grouped by (kernel kind, shape)
+    groups = {}
     if rank == 0:
         ops.normalize_u8(frames[0], eng.x0)
+        eng.serial_side = True
+        eng.forward()                       # warm (no graph)
         ops.profile_begin()
         eng.forward()
         rec = ops.profile_end()
-        for kind, flops, ms in rec:
-            k = kern.setdefault(kind, {"launches": 0, "ms": 0.0, "flop": 0.0})
+        eng.serial_side = False
+        for kind, flops, shape, ms in rec:
+            k = groups.setdefault((kind, shape), {"launches": 0, "ms": 0.0, "flop": 0.0})
             k["launches"] += 1
             k["ms"] += ms
             k["flop"] += flops
-        for k in kern.values():
-            k["tflops"] = k["flop"] / (k["ms"] * 1e-3) / 1e12 if k["ms"] > 0 else None
-            k["avg_us"] = 1000.0 * k["ms"] / k["launches"]
 
     if rank == 0:
         achieved = fps_per_gpu * FLOP_PER_FRAME / 1e12
-        g = kern.get("gemm", {})
+        kern = {}
+        for (kind, shape), g in groups.items():
+            k = kern.setdefault(kind, {"launches": 0, "ms": 0.0, "flop": 0.0})
+            for f in ("launches", "ms", "flop"):
+                k[f] += g[f]
+        for k in kern.values():
+            k["tflops"] = k["flop"] / (k["ms"] * 1e-3) / 1e12 if k["ms"] > 0 else None
+            k["avg_us"] = 1000.0 * k["ms"] / k["launches"]
+        dom_key = max(groups, key=lambda key: groups[key]["ms"])
+        dom = groups[dom_key]
+        dom_avg_us = 1000.0 * dom["ms"] / dom["launches"]
+        dom_flop = dom["flop"] / dom["launches"]
+        dom_tf = dom_flop / (dom_avg_us * 1e-6) / 1e12
+        dom_info = {"kind": dom_key[0], "shape": list(dom_key[1]), "launches_per_frame": dom["launches"],
+                    "avg_us": round(dom_avg_us, 2), "flop_per_launch": dom_flop,
+                    "share_of_frame_kernel_time": round(dom["ms"] / sum(g["ms"] for g in groups.values()), 3)}
+        traffic = None
+        if dom_key[0].startswith("gemm"):
+            M, N, K = dom_key[1]
+            A = torch.empty(8, dtype=eng.dt, device=dev)
+            tile, wgs = ops.gemm(A, A, A, M=M, N=N, K=K, plan_only=True, workspace=eng.ws_main)
+            dom_info["engine"] = {"tile": TILE_NAMES.get(tile, tile), "workgroups": wgs,
+                                  "kernel": TILE_KERNEL.get(tile, "")}
+            traffic = pmc_traffic(TILE_KERNEL.get(tile, "?"), wgs)
+            if traffic is not None:
+                dom_info["traffic_source"] = traffic.pop("source")
         out = {
             "metric": "frames/sec at 1536x1536 (1/2/4/8 MI355X) + depth L1 vs reference",
             "value": round(fps, 3),
@@ -169,13 +220,13 @@ def main():
                                    "DepthPro.infer (patch+image+FOV ViT-L, decoder, heads), hipGraph replay",
                        "global_batch": world, "frame": [1536, 1536], "parallelism": f"frame-dp{world}",
                        "graph": not args.no_graph},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                         "basis": "whole frame: fps_per_gpu x 19.247 TFLOP/frame (SURVEY 8d)",
-                         "dominant_kernel": {"name": "dp_gemm (ViT Linear class)",
-                                             "achieved": round(g.get("tflops") or 0.0, 1),
-                                             "avg_us": round(g.get("avg_us") or 0.0, 2),
-                                             "frac": round((g.get("tflops") or 0.0) / PEAK_BF16_TFLOPS, 4)}},
+            # dominant kernel: algorithmic FLOP per launch / its average HIP-event duration
+            "roofline": {"bound": "mfma", "achieved": round(dom_tf, 1), "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(dom_tf / PEAK_BF16_TFLOPS, 4),
+                         "traffic": traffic["bytes_per_launch"] if traffic else None,
+                         "dominant_kernel": dom_info,
+                         "frame": {"achieved": round(achieved, 1), "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                                   "basis": "fps_per_gpu x 19.247 TFLOP/frame (SURVEY 8d)"}},
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kern.items()},
             "setup_s": round(t_setup, 1),

@@ -37,7 +37,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 1
+#define DP_ABI_VERSION 2
 int dp_abi_version(void);
 
 /*
@@ -99,13 +99,33 @@ typedef struct dp_gemm_args {
   const float* head_w;      /* [N] or NULL */
   float head_b;
   int32_t tile;             /* 0 = auto, else a DP_TILE_* hint */
+  void* workspace;          /* NULL, or >= dp_gemm_workspace_size() bytes of device memory owned by
+                               the caller for THIS stream (never shared by concurrent launches);
+                               enables the persistent stream-K engine for large 256x256-tiled GEMMs */
+  int64_t workspace_bytes;
 } dp_gemm_args;
 
 enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32 = 3,
        DP_TILE_BIG_256x256 = 4, DP_TILE_BIG_256x128 = 5, DP_TILE_BIG_256x256_K32 = 6,
-       DP_TILE_BIG_256x128_K32 = 7, DP_TILE_8PH_256x256 = 8 };
+       DP_TILE_BIG_256x128_K32 = 7, DP_TILE_8PH_256x256 = 8, DP_TILE_DEEP4_256x256 = 9,
+       DP_TILE_DEEP5_256x256 = 10, DP_TILE_DEEP_256x128 = 11, DP_TILE_STREAMK_256x256 = 12,
+       DP_TILE_BIG_320x256 = 13 };
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
+
+/*
+ * Bytes of workspace the stream-K engine needs (flags + one fp32 256x256 partial
+ * tile per persistent workgroup).  Zeroed by dp_gemm itself (a memset node on
+ * the same stream) before each stream-K launch; contents are scratch.
+ */
+int64_t dp_gemm_workspace_size(void);
+
+/*
+ * Which engine / tile and how many workgroups dp_gemm would launch for `args`
+ * (no launch): *tile receives a DP_TILE_* value (DP_TILE_STREAMK_256x256 for the
+ * persistent engine), *grid the workgroup count.  For tests and the bench.
+ */
+int dp_gemm_plan(const dp_gemm_args* args, int32_t* tile, int32_t* grid);
 
 /*
  * dp_layernorm: y[r] = LN(x[r]) * w + b over `cols`, fp32 in, 16-bit out.

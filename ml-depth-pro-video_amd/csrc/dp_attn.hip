@@ -34,19 +34,29 @@ __device__ __forceinline__ int v_off(int row, int byte) {  // byte offset of (ke
 
 template <typename K_>
 __global__ void __launch_bounds__(256, 3)
-attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, float sl2) {
+attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
   __shared__ __attribute__((aligned(16))) u16 sk[2][KT * KS];
   __shared__ __attribute__((aligned(16))) char sv[2][KT * VRB];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = blockIdx.y, b = blockIdx.z;
+  // XCD-aware remap: workgroup i is dispatched to XCD i % 8, so consecutive work
+  // items are handed to the SAME XCD; the nq query blocks of one (image, head),
+  // consecutive here, then share that head's K/V panel in one L2 instead of
+  // fetching it nq times from the fabric (measured: 455 -> ~130 MB per launch).
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int qblk = wid % nq, bh = wid / nq;
+  const int h = bh % heads, b = bh / heads;
   const long long ldq = 3LL * heads * HD;
   const long long ldo = (long long)heads * HD;
   const u16* base = qkv + (long long)b * seq * ldq;
   const int qcol = h * HD, kcol = heads * HD + h * HD, vcol = 2 * heads * HD + h * HD;
 
   const int l32 = lane & 31, hi = lane >> 5;
-  const int q = blockIdx.x * QB + wave * 32 + l32;
+  const int q = qblk * QB + wave * 32 + l32;
+  // a wave whose 32 queries are all past seq (tail block) only helps stage K/V
+  const bool active = __builtin_amdgcn_readfirstlane(qblk * QB + wave * 32) < seq;
 
   // Q fragments (B operand of S^T = K Q^T): Q[q][16*ks + 8*hi + 0..7]
   uint4 qf[4];
@@ -105,6 +115,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   // are masked, and the second 32-key half is skipped when it holds none.
   auto do_tile = [&](int t, auto partial_tag) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
+    if (!active) return;
     const int cur = t & 1;
     const int kbase = t * KT;
     const u16* K = sk[cur];
@@ -223,7 +234,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = i * 8 + (lane >> 3), ch = lane & 7;
-    const int qq = blockIdx.x * QB + wave * 32 + row;
+    const int qq = qblk * QB + wave * 32 + row;
     const uint4 v = *(const uint4*)(stg + row * KS + 8 * ch);
     if (qq < seq) *(uint4*)(out + ((long long)b * seq + qq) * ldo + h * HD + 8 * ch) = v;
   }
@@ -235,14 +246,15 @@ extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t s
                             int32_t head_dim, float scale, int32_t dtype, dp_stream_t stream) {
   if (!qkv || !out) return DP_ERR_ARG;
   if (batch <= 0 || seq <= 0 || heads <= 0 || head_dim != HD) return DP_ERR_SHAPE;
-  if (batch > 65535 || heads > 65535) return DP_ERR_SHAPE;
-  dim3 grid((seq + QB - 1) / QB, heads, batch);
+  const int nq = (seq + QB - 1) / QB;
+  if ((long long)nq * heads * batch > 0x7fffffffLL) return DP_ERR_SHAPE;
+  dim3 grid(nq * heads * batch);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DP_BF16)
-    hipLaunchKernelGGL(attn_kernel<KBF16>, grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, sl2);
+    hipLaunchKernelGGL(attn_kernel<KBF16>, grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
   else if (dtype == DP_F16)
-    hipLaunchKernelGGL(attn_kernel<KF16>, grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, sl2);
+    hipLaunchKernelGGL(attn_kernel<KF16>, grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
   else
     return DP_ERR_DTYPE;
   DP_CHECK_LAUNCH();

@@ -53,11 +53,29 @@ struct GemmP {
   int row_group, row_group_out, row_off;
   const float* head_w;
   float head_b;
-  int tiles_n;
+  int tiles_n, tiles_m;
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
 };
 
 int g_dbg_flags = 0;
+
+// persistent workgroups of the stream-K engine: one per CU, at most one per tile
+int g_num_cu = 0;
+int num_cus() {
+  if (g_num_cu == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_num_cu = n;
+  }
+  return g_num_cu;
+}
+int sk_grid(const GemmP& p) {
+  const int tiles = p.tiles_m * p.tiles_n;
+  int g = num_cus();
+  if (g > 256) g = 256;   // == SK_MAX_WG (workspace slots)
+  return tiles < g ? tiles : g;
+}
 
 #ifdef DP_STAMPS
 // Timing-only builds (make stamps): per-workgroup s_memrealtime (100 MHz) stamps
@@ -418,11 +436,10 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
   }
 }
 
-template <typename K_, int BN, int BKT, int NS, bool CONV, bool RELU>
+template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU>
 __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
-  constexpr int BM = 256;
   constexpr int WN = 4;
-  constexpr int TM = 128, TN = BN / WN;
+  constexpr int TM = BM / 2, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int RB = BKT * 2;                 // LDS row bytes
   constexpr int CR = BKT / 8;                 // 16-B chunks per row
@@ -534,20 +551,29 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   };
 
   const int KT = p.K / BKT;
-  if constexpr (NS == 2) {
-    // 2-stage ring, one barrier per K step.  Top of iteration kt: tile kt is in
-    // flight; wait for it, then the barrier makes it visible to every wave AND
-    // certifies that every wave finished compute(kt-1), whose stage is refilled
-    // with tile kt+1 right away -- one step of MFMA work covers each load.
-    issue(0, 0);
+  auto nxt = [&](int st) { return st + 1 == NS ? 0 : st + 1; };
+  // wait until tile t has landed: tiles issued so far are 0 .. min(KT-1, t+NS-2)
+  auto wait_tile = [&](int t) { wait_vmcnt_le<(NS - 2) * LT>(min(NS - 2, KT - 1 - t) * LT); };
+  if constexpr (!PIPE) {
+    // NS-stage ring, one barrier per K step.  Top of iteration kt: tiles kt ..
+    // kt+NS-2 are in flight; wait for tile kt only (counted vmcnt), then the
+    // barrier makes it visible to every wave AND certifies that every wave
+    // finished compute(kt-1), whose stage is refilled with tile kt+NS-1 right
+    // away -- NS-1 steps of MFMA work cover each load.
+    #pragma unroll
+    for (int t = 0; t < NS - 1; ++t)
+      if (t < KT) issue(t, t);
     int stage = 0;
     for (int kt = 0; kt < KT; ++kt) {
-      wait_vmcnt<0>();
+      wait_tile(kt);
       lds_barrier();
 #ifdef DP_STAMPS
       if (kt == 0) DP_STAMP(st1_);
 #endif
-      if (kt + 1 < KT && !(p.dbg & 2)) issue(kt + 1, stage ^ 1);
+      if (kt + NS - 1 < KT && !(p.dbg & 2)) {
+        const int st = stage + NS - 1;
+        issue(kt + NS - 1, st >= NS ? st - NS : st);
+      }
       if (p.dbg & 4) {
         const u16* sa = (const u16*)(smem + stage * STAGE);
         uint4 t = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + frow, fchunk));
@@ -555,7 +581,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       } else {
         compute(stage);
       }
-      stage ^= 1;
+      stage = nxt(stage);
     }
   } else {
     // NS >= 3: software-pipelined.  The fragments of the next k sub-step (or of
@@ -584,9 +610,6 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       }
       __builtin_amdgcn_s_setprio(0);
     };
-    auto nxt = [&](int st) { return st + 1 == NS ? 0 : st + 1; };
-    // wait until tile t has landed: tiles issued so far are 0 .. min(KT-1, t+NS-2)
-    auto wait_tile = [&](int t) { wait_vmcnt_le<(NS - 2) * LT>(min(NS - 2, KT - 1 - t) * LT); };
     #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
       if (t < KT) issue(t, t);
@@ -816,6 +839,12 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
     wait_vmcnt<0>();
   }
   lds_barrier();
+  // Wave rows run staggered by one barrier: while one wave of a SIMD waits on
+  // its fragment reads the other issues MFMAs.  Every LDS-DMA wait therefore
+  // sits one phase before the first read of what it retires (phase 3 for the
+  // next K tile, read from phase 0 on), so both wave groups have passed their
+  // wait before either reads.
+  if (wm == 1) bar();
   for (int t = 0; t < KT; ++t) {
     const int buf = t & 1;
     const bool n1 = t + 1 < KT, n2 = t + 2 < KT;
@@ -831,17 +860,21 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
     readA(1, buf);
     if (n2) issueB(0, t + 2);
     bar(); mma(1, 0); bar();
-    // phase 3: quadrant (1,1); then tile t+1 must have landed
+    // phase 3: quadrant (1,1); tile t+1 must have landed before this phase's first barrier
+    if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>();
     if (n2) issueB(1, t + 2);
     bar(); mma(1, 1);
-    if (n2) wait_vmcnt<4>(); else wait_vmcnt<0>();
     bar();
   }
+  if (wm == 0) bar();
 
   // epilogue: identical to the big engine (LDS-staged, row-coalesced)
   lds_barrier();
-  constexpr int SROW = TN + 4, CPR = TN / 8, RPI = 64 / CPR;
+  constexpr int SROW = TN + 4, CPR = TN / 8, RPI = 64 / CPR, NIT = 32 / RPI;
   float* stg = (float*)smem + wave * (32 * SROW);
+  const int c8 = (lane % CPR) * 8, n_l = n0 + wn * TN + c8;
+  ColConst cc;
+  load_colconst(p, n_l, cc);
   #pragma unroll
   for (int q = 0; q < 4; ++q) {
     #pragma unroll
@@ -849,15 +882,18 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
       #pragma unroll
       for (int j = 0; j < 4; ++j)
         *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[2 * q + i][j];
+    float v[NIT][8];
+    int ms[NIT];
     #pragma unroll
-    for (int r0 = 0; r0 < 32; r0 += RPI) {
-      const int row = r0 + lane / CPR, c8 = (lane % CPR) * 8;
+    for (int it = 0; it < NIT; ++it) {
+      const int row = it * RPI + lane / CPR;
       const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
       const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
-      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const int m = m0 + wm * TM + q * 32 + row, n = n0 + wn * TN + c8;
-      if (m < p.M && n < p.N) epilogue8<K_>(p, m, n, v);
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
+      ms[it] = m0 + wm * TM + q * 32 + row;
     }
+    epilogue_rows<K_, NIT>(p, cc, ms, n_l, v);
   }
 }
 
@@ -870,6 +906,297 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
   else if (conv) hipLaunchKernelGGL((gemm_8ph_kernel<K_, true, false>), grid, dim3(512), 0, s, p);
   else if (p.relu_a) hipLaunchKernelGGL((gemm_8ph_kernel<K_, false, true>), grid, dim3(512), 0, s, p);
   else hipLaunchKernelGGL((gemm_8ph_kernel<K_, false, false>), grid, dim3(512), 0, s, p);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+
+// ================================================= stream-K persistent engine
+// 256 x 256 x 64 tiles, 8 waves (2 x 4, wave tile 128 x 64), one persistent
+// workgroup per CU.  The T tiles x KT k-steps of the GEMM form one list of
+// "units" (tile-major, k inner) that is cut into G equal contiguous ranges,
+// one per workgroup (stream-K), so that
+//  * every CU gets the same work (no 3.7-round quantisation tail),
+//  * the LDS-DMA ring runs on across tile boundaries: the next tile's first
+//    k-step is in flight while the previous tile's epilogue runs (no prologue
+//    per tile), and
+//  * tile boundaries -- hence the epilogue store bursts -- fall at different
+//    times on different CUs instead of all 256 CUs storing at once.
+// A range that starts inside a tile computes that tile's last k-steps and
+// publishes them as an fp32 partial (write-through stores + flag); the
+// workgroup whose range covers the tile's k-step 0 (it reaches it at the END
+// of its range) owns the tile: it adds every partial of the tile, then runs the
+// normal epilogue.  A workgroup only ever waits for a higher-numbered one,
+// which published at the START of its range: no cycle, no deadlock, and the
+// spin is bounded (a timeout sets an error word instead of hanging the GPU).
+// The epilogue stages 16-row slices through its own 32 KiB of LDS so that the
+// 128 KiB ring stays live underneath it.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int SK_A_BYTES = 256 * 128;            // 256 rows x 64 16-bit
+constexpr int SK_STAGE = 2 * SK_A_BYTES;         // A + B
+constexpr int SK_RING = 2 * SK_STAGE;            // 2 stages: 128 KiB
+constexpr int SK_EPI = 8 * 16 * 64 * 4;          // 8 waves x 16 rows x 64 fp32
+constexpr int SK_TILE_F = 256 * 256;             // floats per partial slot
+constexpr long long SK_FLAG_BYTES = 4096;        // flags [0, G), error word at [1023]
+constexpr int SK_MAX_WG = 256;
+
+struct SkP {
+  uint32_t* flags;
+  float* part;
+  int kt, tiles, units;
+};
+
+// ROWLD: the epilogue reads per-row operands (residuals R1/R2, the fp32 C being
+// accumulated into, pos-embed); without them it needs ~40 fewer VGPRs.
+template <typename K_, bool CONV, bool RELU, bool ROWLD>
+__global__ void __launch_bounds__(512, 1) gemm_sk_kernel(const GemmP p, const SkP s) {
+  constexpr int TM = 128, TN = 64, FM = 8, FN = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[SK_RING + SK_EPI];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int KT = s.kt, U = s.units;
+  const int u0 = (int)((long long)w * U / G), u1 = (int)((long long)(w + 1) * U / G);
+  auto wg_of_unit = [&](int u) { return (int)(((long long)(u + 1) * G - 1) / U); };
+  // Tile positions are walked column-major over an R x G grid of tile ids
+  // (id = row * G + column): range w then covers ~column w, i.e. tiles w, w+G,
+  // w+2G, ... as in a data-parallel launch, so the tiles in flight at any
+  // moment are ~consecutive ids (shared A/B panels in L2), while the fractional
+  // range length staggers the tile boundaries across workgroups.
+  const int T = s.tiles, R = (T + G - 1) / G, r0 = T - (R - 1) * G;
+  auto tile_of = [&](int pos) {
+    int c, r;
+    if (pos < r0 * R) {
+      c = pos / R;
+      r = pos - c * R;
+    } else {
+      const int q = pos - r0 * R;
+      c = r0 + q / (R - 1);
+      r = q - (c - r0) * (R - 1);
+    }
+    return r * G + c;
+  };
+
+  // ---- LDS-DMA issue side (runs one unit ahead of the MFMAs).  Only the
+  // tile's scalar origin is kept: per-lane source addresses are recomputed per
+  // issue (a few VALU ops under 64 MFMAs) so the 128 accumulators, the
+  // fragments and the epilogue fit in 256 VGPRs without spilling.
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  int is_tile = -1, is_m0 = 0, is_n0 = 0;
+  ConvRow a_cr[CONV ? 4 : 1];
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
+  auto issue = [&](int u, int stage) {
+    const int t = u / KT, ks = u - t * KT;
+    if (t != is_tile) {
+      is_tile = t;
+      const int id = tile_of(t);
+      is_m0 = (id / p.tiles_n) * 256;
+      is_n0 = (id % p.tiles_n) * 256;
+      if constexpr (CONV) {
+        #pragma unroll
+        for (int i = 0; i < 4; ++i) a_cr[i] = conv_row(p, is_m0 + i * 64 + prow);
+      }
+    }
+    const uint32_t sa = lds_base + stage * SK_STAGE, sb = sa + SK_A_BYTES;
+    const int k0 = ks * 64;
+    int ky = 0, kx = 0, ci = 0;
+    if constexpr (CONV) {
+      const int tap = k0 / p.in_c;
+      ci = k0 - tap * p.in_c;
+      ky = tap / p.k_w;
+      kx = tap - ky * p.k_w;
+    }
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const void* src;
+      if constexpr (CONV) {
+        bool inb;
+        const u16* q = conv_src(p, a_cr[i], ky, kx, ci + pchunk * 8, inb);
+        src = inb ? (const void*)q : (const void*)g_zero_page;
+      } else {
+        const int m = is_m0 + i * 64 + prow;
+        src = p.A + (long long)(m < p.M ? m : p.M - 1) * p.lda + k0 + pchunk * 8;
+      }
+      glds16(src, sa + i * 8192);
+    }
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = is_n0 + i * 64 + prow;
+      glds16(p.B + (long long)(n < p.N ? n : p.N - 1) * p.ldb + k0 + pchunk * 8, sb + i * 8192);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+  auto zero_acc = [&]() {
+    #pragma unroll
+    for (int i = 0; i < FM; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  };
+  const int frow = lane & 15, fchunk = lane >> 4;
+  auto compute = [&](int stage) {
+    const u16* sa = (const u16*)(smem + stage * SK_STAGE);
+    const u16* sb = (const u16*)(smem + stage * SK_STAGE + SK_A_BYTES);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 bf[FN];
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *(const uint4*)(sb + lds_off(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      __builtin_amdgcn_s_setprio(1);
+      #pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        uint4 af = *(const uint4*)(sa + lds_off(wm * TM + i * 16 + frow, ks * 4 + fchunk));
+        if constexpr (RELU) af = relu_pk16(af);
+        #pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  // ---- epilogue of one finished tile: 16-row slices through this wave's LDS slab,
+  // read back row-major (8 rows x 8 columns per lane instruction pair)
+  float* stg = (float*)(smem + SK_RING) + wave * (16 * 64);
+  auto epilogue = [&](int t) {
+    const int id = tile_of(t);
+    const int m0 = (id / p.tiles_n) * 256, n0 = (id % p.tiles_n) * 256;
+    const int c8 = (lane & 7) * 8, n_l = n0 + wn * TN + c8;
+    ColConst cc;                     // bias / LayerScale of this lane's 8 columns, loaded once
+    load_colconst(p, n_l, cc);
+    #pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      // lane holds row (lane & 15), 16-B chunks j*4 + (lane >> 4); chunk index XOR row
+      #pragma unroll
+      for (int j = 0; j < FN; ++j)
+        *(f32x4_t*)(stg + frow * 64 + (((j * 4 + fchunk) ^ frow) << 2)) = acc[i][j];
+      float v[2][8];
+      int ms[2];
+      #pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int row = it * 8 + (lane >> 3);
+        const f32x4_t lo = *(const f32x4_t*)(stg + row * 64 + (((2 * (lane & 7)) ^ row) << 2));
+        const f32x4_t hi = *(const f32x4_t*)(stg + row * 64 + (((2 * (lane & 7) + 1) ^ row) << 2));
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
+        ms[it] = m0 + wm * TM + i * 16 + row;
+      }
+      if constexpr (ROWLD) {
+        epilogue_rows<K_, 2>(p, cc, ms, n_l, v);   // both rows' loads issued before any math
+      } else {
+        GemmP q = p;
+        q.R1 = nullptr; q.R2 = nullptr; q.pos = nullptr; q.accumulate = 0;
+        epilogue_rows<K_, 2>(q, cc, ms, n_l, v);
+      }
+    }
+  };
+
+  // partial slot layout: [wave][i][j][lane] x f32x4 -> 1 KiB contiguous per wave instruction
+  auto slot_ptr = [&](int q, int i, int j) {
+    return s.part + (long long)q * SK_TILE_F + ((((wave * FM + i) * FN + j) * 64 + lane) << 2);
+  };
+  auto publish = [&]() {
+    // write-through (sc1) 16-B buffer stores of this wave's accumulators into slot w:
+    // visible to the owner after its agent-scope acquire (Guideline 16, R1)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(s.part + (long long)w * SK_TILE_F, (short)0, SK_TILE_F * 4, 0x00020000);
+    const int vo = (wave * FM * FN * 64 + lane) * 16;
+    #pragma unroll
+    for (int i = 0; i < FM; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), rs, vo + (i * FN + j) * 1024, 0,
+                                               16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its stores
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(s.flags + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto absorb = [&](int q) {   // add workgroup q's published partial of the tile
+    if (tid == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(s.flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {  // ~seconds: never hang the GPU; report instead
+          __hip_atomic_store(s.flags + 1023, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    #pragma unroll
+    for (int i = 0; i < FM; ++i) {   // one fragment row at a time (bounded live registers)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] += *(const f32x4_t*)slot_ptr(q, i, j);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  if (u0 >= u1) return;
+  zero_acc();
+  issue(u0, 0);
+  int stage = 0, seg0 = u0;
+  int t = u0 / KT, ks = u0 - t * KT;
+  for (int u = u0; u < u1; ++u) {
+    wait_vmcnt<0>();
+    lds_barrier();
+    if (u + 1 < u1) issue(u + 1, stage ^ 1);
+    compute(stage);
+    stage ^= 1;
+    if (ks == KT - 1 || u + 1 == u1) {
+      const bool head = seg0 == t * KT;
+      if (!head) {
+        publish();                       // only ever this range's first segment
+      } else {
+        if (ks != KT - 1) {              // split tile, owned here: the range's last segment
+          const int last = wg_of_unit(t * KT + KT - 1);
+          for (int q = w + 1; q <= last; ++q) absorb(q);
+        }
+        epilogue(t);
+      }
+      zero_acc();
+      seg0 = u + 1;
+      ++t;
+      ks = 0;
+    } else {
+      ++ks;
+    }
+  }
+}
+
+template <typename K_>
+int launch_sk(const GemmP& p0, bool conv, void* ws, hipStream_t st) {
+  GemmP p = p0;
+  SkP s;
+  s.kt = p.K / 64;
+  s.tiles = p.tiles_m * p.tiles_n;
+  s.units = s.tiles * s.kt;
+  const int G = sk_grid(p);
+  s.flags = (uint32_t*)ws;
+  s.part = (float*)((char*)ws + SK_FLAG_BYTES);
+  hipError_t e = hipMemsetAsync(ws, 0, SK_FLAG_BYTES, st);
+  if (e != hipSuccess) return (int)e;
+  dim3 grid(G);
+  const bool rowld = p.R1 || p.R2 || p.pos || p.accumulate;
+#define DP_SK(C_, R_, L_) hipLaunchKernelGGL((gemm_sk_kernel<K_, C_, R_, L_>), grid, dim3(512), 0, st, p, s)
+  if (rowld) {
+    if (conv && p.relu_a) DP_SK(true, true, true);
+    else if (conv) DP_SK(true, false, true);
+    else if (p.relu_a) DP_SK(false, true, true);
+    else DP_SK(false, false, true);
+  } else {
+    if (conv && p.relu_a) DP_SK(true, true, false);
+    else if (conv) DP_SK(true, false, false);
+    else if (p.relu_a) DP_SK(false, true, false);
+    else DP_SK(false, false, false);
+  }
+#undef DP_SK
   DP_CHECK_LAUNCH();
   return 0;
 }
@@ -1030,24 +1357,22 @@ int launch_small(const GemmP& p0, bool conv, hipStream_t s) {
   return 0;
 }
 
-template <typename K_, int BN, int BKT>
+// NS = ring depth; PIPE = software-pipelined fragment reads (two register sets:
+// only affordable for BN = 128, the 256x256 accumulators leave no room).
+template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE>
 int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   GemmP p = p0;
   p.tiles_n = (p.N + BN - 1) / BN;
-  const int tiles_m = (p.M + 255) / 256;
-  dim3 grid(p.tiles_n * tiles_m);
-  // ring depth: as deep as LDS allows for 256x128 (software-pipelined loop); the
-  // 256x256 tile keeps 2 stages (its double fragment set would not fit 256 VGPRs)
-  constexpr int NS_MAX = (160 * 1024) / ((256 + BN) * BKT * 2) > 6 ? 6 : (160 * 1024) / ((256 + BN) * BKT * 2);
-  constexpr int NS = BN == 256 ? 2 : NS_MAX;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  dim3 grid(p.tiles_n * p.tiles_m);
   if (conv && p.relu_a)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, true, true>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, true, true>), grid, dim3(NT_BIG), 0, s, p);
   else if (conv)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, true, false>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, true, false>), grid, dim3(NT_BIG), 0, s, p);
   else if (p.relu_a)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, false, true>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, true>), grid, dim3(NT_BIG), 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BN, BKT, NS, false, false>), grid, dim3(NT_BIG), 0, s, p);
+    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, false>), grid, dim3(NT_BIG), 0, s, p);
   DP_CHECK_LAUNCH();
   return 0;
 }
@@ -1058,11 +1383,15 @@ int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
     case DP_TILE_256x64: return launch_small<K_, 256, 64, 4, 1>(p, conv, s);
     case DP_TILE_256x32: return launch_small<K_, 256, 32, 4, 1>(p, conv, s);
     case DP_TILE_128x128: return launch_small<K_, 128, 128, 2, 2>(p, conv, s);
-    case DP_TILE_BIG_256x128: return launch_big<K_, 128, 64>(p, conv, s);
-    case DP_TILE_BIG_256x128_K32: return launch_big<K_, 128, 32>(p, conv, s);
-    case DP_TILE_BIG_256x256_K32: return launch_big<K_, 256, 32>(p, conv, s);
+    case DP_TILE_BIG_256x128: return launch_big<K_, 256, 128, 64, 3, true>(p, conv, s);
+    case DP_TILE_BIG_256x128_K32: return launch_big<K_, 256, 128, 32, 6, true>(p, conv, s);
+    case DP_TILE_BIG_256x256_K32: return launch_big<K_, 256, 256, 32, 2, false>(p, conv, s);
     case DP_TILE_8PH_256x256: return launch_8ph<K_>(p, conv, s);
-    default: return launch_big<K_, 256, 64>(p, conv, s);
+    case DP_TILE_DEEP4_256x256: return launch_big<K_, 256, 256, 32, 4, false>(p, conv, s);
+    case DP_TILE_DEEP5_256x256: return launch_big<K_, 256, 256, 32, 5, false>(p, conv, s);
+    case DP_TILE_DEEP_256x128: return launch_big<K_, 256, 128, 32, 6, false>(p, conv, s);
+    case DP_TILE_BIG_320x256: return launch_big<K_, 320, 256, 64, 2, false>(p, conv, s);
+    default: return launch_big<K_, 256, 256, 64, 2, false>(p, conv, s);
   }
 }
 
@@ -1080,7 +1409,11 @@ extern "C" int dp_gemm_debug_flags(int flags) {
   return 0;
 }
 
-extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
+extern "C" int64_t dp_gemm_workspace_size(void) { return SK_FLAG_BYTES + (int64_t)SK_MAX_WG * SK_TILE_F * 4; }
+
+namespace {
+// Validate the arguments, fill the kernel parameters and pick the engine.
+int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   if (!a) return DP_ERR_ARG;
   if (a->M <= 0 || a->N <= 0 || a->K <= 0) return DP_ERR_SHAPE;
   if (a->K % BK != 0 || a->N % 4 != 0) return DP_ERR_SHAPE;
@@ -1101,27 +1434,38 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
         a->M % (a->dc_h * a->dc_w) != 0)
       return DP_ERR_SHAPE;
   }
-  int tile = a->tile;
+  const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
+  tile = a->tile;
   if (a->head_w) {
     if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;
     tile = DP_TILE_256x32;
   }
+  const long long tiles256 = (long long)((a->M + 255) / 256) * (a->N / 256);
+  if (tile == DP_TILE_STREAMK_256x256 && (!ws_ok || a->N % 256 != 0)) return DP_ERR_ARG;
   if (tile == DP_TILE_AUTO) {
     if (a->N <= 32) tile = DP_TILE_256x32;
     else if (a->N <= 64) tile = DP_TILE_256x64;
     else if (a->N % 8 != 0) tile = DP_TILE_128x128;
+    else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
     else {
-      // 256x256 halves operand traffic per FLOP but needs enough tiles to keep
-      // 256 CUs busy through the last wave of workgroups (measured crossover
-      // ~600 tiles on the ViT / decoder shapes: tools/gemm_bench.py).
-      const long long tiles256 = (long long)((a->M + 255) / 256) * (a->N / 256);
-      tile = (a->N % 256 == 0 && tiles256 >= 600) ? DP_TILE_BIG_256x256 : DP_TILE_BIG_256x128;
+      // Wide-N GEMMs: 256 x 256 tiles (8-phase engine once there are >= 600 of
+      // them: tools/gemm_bench.py), or 320 x 256 when that needs fewer rounds of
+      // workgroups over the CUs per unit of tile work -- e.g. the ViT's M = 20195
+      // is exactly 64 tiles of 320 rows, so proj/fc2 (N = 1024) run as ONE round
+      // of 256 tiles instead of 2 rounds of 316.
+      const long long ncu = num_cus();
+      const long long tiles320 = (long long)((a->M + 319) / 320) * (a->N / 256);
+      const long long tiles128 = (long long)((a->M + 255) / 256) * (a->N / 128);
+      // rounds x rows-of-work per tile; the 256x128 engine's loop runs ~15 % slower per FLOP
+      const long long cost256 = (tiles256 + ncu - 1) / ncu * 256 * 20, cost320 = (tiles320 + ncu - 1) / ncu * 320 * 20;
+      const long long cost128 = (tiles128 + ncu - 1) / ncu * 128 * 23;
+      if (cost128 < cost256 && cost128 < cost320) tile = DP_TILE_BIG_256x128;
+      else if (cost320 < cost256) tile = DP_TILE_BIG_320x256;
+      else tile = (tiles256 >= 600 && a->a_mode != DP_A_CONV) ? DP_TILE_8PH_256x256 : DP_TILE_BIG_256x256;
     }
   }
-
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
 
-  GemmP p;
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
   p.B = (const u16*)a->B; p.ldb = a->ldb;
@@ -1136,9 +1480,47 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
   p.row_group = a->row_group; p.row_group_out = a->row_group_out; p.row_off = a->row_off;
   p.head_w = a->head_w; p.head_b = a->head_b;
   p.tiles_n = 1;
+  p.tiles_m = 1;
+  if (tile == DP_TILE_STREAMK_256x256) {
+    p.tiles_n = a->N / 256;
+    p.tiles_m = (a->M + 255) / 256;
+  }
   p.dbg = g_dbg_flags;
+  return 0;
+}
+}  // namespace
+
+extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* grid_out) {
+  GemmP p;
+  int tile = 0;
+  const int rc = gemm_plan(a, p, tile);
+  if (rc) return rc;
+  const int N = a->N, M = a->M;
+  int bm = 256, bn = 128;
+  switch (tile) {
+    case DP_TILE_256x64: bn = 64; break;
+    case DP_TILE_256x32: bn = 32; break;
+    case DP_TILE_128x128: bm = 128; bn = 128; break;
+    case DP_TILE_BIG_256x128: case DP_TILE_BIG_256x128_K32: case DP_TILE_DEEP_256x128: bn = 128; break;
+    case DP_TILE_BIG_320x256: bm = 320; bn = 256; break;
+    default: bn = 256;
+  }
+  if (tile_out) *tile_out = tile;
+  if (grid_out) *grid_out = tile == DP_TILE_STREAMK_256x256 ? sk_grid(p) : ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  return 0;
+}
+
+extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
+  GemmP p;
+  int tile = 0;
+  const int rc = gemm_plan(a, p, tile);
+  if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   const bool conv = a->a_mode == DP_A_CONV;
+  if (tile == DP_TILE_STREAMK_256x256) {
+    if (a->dtype == DP_BF16) return launch_sk<KBF16>(p, conv, a->workspace, s);
+    return launch_sk<KF16>(p, conv, a->workspace, s);
+  }
   if (a->dtype == DP_BF16) return launch_k<KBF16>(p, tile, conv, s);
   return launch_k<KF16>(p, tile, conv, s);
 }

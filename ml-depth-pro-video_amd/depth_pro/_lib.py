@@ -18,8 +18,9 @@ DP_ACT_NONE, DP_ACT_RELU, DP_ACT_GELU = 0, 1, 2
 DP_A_DENSE, DP_A_CONV = 0, 1
 DP_STORE_ROWS, DP_STORE_DECONV2X2 = 0, 1
 (DP_TILE_AUTO, DP_TILE_128x128, DP_TILE_256x64, DP_TILE_256x32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x128,
- DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256) = range(9)
-DP_ABI_VERSION = 1
+ DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
+ DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256) = range(14)
+DP_ABI_VERSION = 2
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -31,7 +32,7 @@ LIB_PATH = os.environ.get(
 EXPORTS = (
     "dp_abi_version", "dp_gemm", "dp_layernorm", "dp_attention", "dp_normalize_u8",
     "dp_resize_bilinear", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
-    "dp_fov_tail", "dp_infer_epilogue",
+    "dp_fov_tail", "dp_infer_epilogue", "dp_gemm_workspace_size", "dp_gemm_plan",
 )
 
 
@@ -60,6 +61,7 @@ class GemmArgs(ctypes.Structure):
         ("row_group", ctypes.c_int32), ("row_group_out", ctypes.c_int32), ("row_off", ctypes.c_int32),
         ("head_w", ctypes.c_void_p), ("head_b", ctypes.c_float),
         ("tile", ctypes.c_int32),
+        ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
     ]
 
 
@@ -98,11 +100,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "dp_merge_windows": [vp, i32, i64, i32, i32, i32, vp, i32, vp],
         "dp_fov_tail": [vp, i32, vp, f32, vp, vp],
         "dp_infer_epilogue": [vp, i32, i32, vp, i32, f64, i32, i32, vp, vp, vp],
+        "dp_gemm_workspace_size": [],
+        "dp_gemm_plan": [ctypes.POINTER(GemmArgs), ctypes.POINTER(i32), ctypes.POINTER(i32)],
     }
     for name, argtypes in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
+    lib.dp_gemm_workspace_size.restype = ctypes.c_int64
     ver = lib.dp_abi_version()
     if ver != DP_ABI_VERSION:
         raise DPError(f"{path} has ABI version {ver}, expected {DP_ABI_VERSION}; rebuild it")

@@ -210,6 +210,10 @@ class Engine:
         self.fov_deg = e(1, 1, 1, 1, dtype=torch.float32)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.side = torch.cuda.Stream(device=dev)
+        # stream-K GEMM scratch, one per stream that issues GEMMs (main / side)
+        self.ws_main = ops.gemm_workspace(dev)
+        self.ws_side = ops.gemm_workspace(dev)
+        self.serial_side = False   # True: run the side encoders on the current stream (profiling)
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
@@ -293,7 +297,12 @@ class Engine:
             ops.gemm(vf.h, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
 
     def forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Run the network on `self.x0`; results in self.canonical / self.fov_deg.
+        """Run the network on `self.x0`; results in self.canonical / self.fov_deg."""
+        with ops.use_workspace(self.ws_main):
+            return self._forward()
+
+    def _forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Body of `forward`.
 
         Two streams: the current stream runs the patch encoder -> decoder -> head;
         `self.side` runs the image + FOV encoders (forked after the window
@@ -302,10 +311,13 @@ class Engine:
         P = self.P
         main = torch.cuda.current_stream(self.dev)
         ops.patchify_pyramid(self.x0, self.cols)
-        self.side.wait_stream(main)
-        with torch.cuda.stream(self.side):
-            if "side" not in _ABLATE:
-                self._side_encoders()
+        if self.serial_side:
+            self._side_encoders()
+        else:
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side), ops.use_workspace(self.ws_side):
+                if "side" not in _ABLATE:
+                    self._side_encoders()
         vp = self.vp
         hooks = {
             5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
@@ -330,7 +342,8 @@ class Engine:
         self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
         ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
-        main.wait_stream(self.side)  # join: image-encoder half of `cat` and fov tokens ready
+        if not self.serial_side:
+            main.wait_stream(self.side)  # join: image-encoder half of `cat` and fov tokens ready
         ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
         self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)

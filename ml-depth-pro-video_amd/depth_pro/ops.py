@@ -30,7 +30,7 @@ def dtype_code(dt: torch.dtype) -> int:
     raise _lib.DPError(f"unsupported dtype {dt}")
 
 
-# Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, ev0, ev1).
+# Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, shape, ev0, ev1).
 _PROF: Optional[list] = None
 
 
@@ -40,16 +40,16 @@ def profile_begin() -> None:
 
 
 def profile_end() -> list:
-    """Stop recording; returns [(kind, flops, milliseconds)] (synchronizes)."""
+    """Stop recording; returns [(kind, flops, shape, milliseconds)] (synchronizes)."""
     global _PROF
     rec, _PROF = _PROF or [], None
     torch.cuda.synchronize()
-    return [(k, f, a.elapsed_time(b)) for (k, f, a, b) in rec]
+    return [(k, f, sh, a.elapsed_time(b)) for (k, f, sh, a, b) in rec]
 
 
 class _Timed:
-    def __init__(self, kind: str, flops: float):
-        self.kind, self.flops = kind, flops
+    def __init__(self, kind: str, flops: float, shape: tuple = ()):
+        self.kind, self.flops, self.shape = kind, flops, shape
 
     def __enter__(self):
         if _PROF is not None:
@@ -61,8 +61,35 @@ class _Timed:
     def __exit__(self, *exc):
         if _PROF is not None:
             self.e1.record()
-            _PROF.append((self.kind, self.flops, self.e0, self.e1))
+            _PROF.append((self.kind, self.flops, self.shape, self.e0, self.e1))
         return False
+
+
+# Stream-K workspace for the GEMMs issued inside `use_workspace(ws)` (one per
+# stream that may run a GEMM concurrently with another; see Engine).
+_WS: Optional[torch.Tensor] = None
+
+
+class use_workspace:
+    """Context manager: GEMMs issued inside it may use the persistent stream-K engine with `ws`."""
+
+    def __init__(self, ws: Optional[torch.Tensor]):
+        self.ws = ws
+
+    def __enter__(self):
+        global _WS
+        self.prev, _WS = _WS, self.ws
+        return self
+
+    def __exit__(self, *exc):
+        global _WS
+        _WS = self.prev
+        return False
+
+
+def gemm_workspace(device: torch.device) -> torch.Tensor:
+    """A zeroed device buffer of dp_gemm_workspace_size() bytes."""
+    return torch.zeros(int(_lib.load().dp_gemm_workspace_size()), dtype=torch.uint8, device=device)
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -84,8 +111,13 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          accumulate: bool = False, deconv: Optional[tuple] = None,
          row_group: int = 0, row_group_out: int = 0, row_off: int = 0,
          head_w: Optional[torch.Tensor] = None, head_b: float = 0.0,
-         A_off: int = 0, C_off: int = 0, tile: int = 0) -> None:
-    """dp_gemm. `A_off`/`C_off` are element offsets into A / C (sub-views)."""
+         A_off: int = 0, C_off: int = 0, tile: int = 0, workspace: Optional[torch.Tensor] = None,
+         plan_only: bool = False):
+    """dp_gemm. `A_off`/`C_off` are element offsets into A / C (sub-views).
+
+    `workspace` (or the one set by `use_workspace`) enables the stream-K engine.
+    `plan_only=True` launches nothing and returns (tile, workgroups) from dp_gemm_plan.
+    """
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.dtype = dtype_code(B.dtype)
@@ -123,21 +155,28 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     a.head_w = _p(head_w)
     a.head_b = float(head_b)
     a.tile = tile
+    ws = workspace if workspace is not None else _WS
+    if ws is not None:
+        a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * ws.element_size()
+    if plan_only:
+        t, g = ctypes.c_int32(), ctypes.c_int32()
+        check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
+        return t.value, g.value
     kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
-    with _Timed(kind, 2.0 * M * N * K):
+    with _Timed(kind, 2.0 * M * N * K, (M, N, K)):
         check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
 
 
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor, rows: int, cols: int,
               eps: float = 1e-6) -> None:
-    with _Timed("layernorm", 0.0):
+    with _Timed("layernorm", 0.0, (rows, cols)):
         check(_lib.load().dp_layernorm(x.data_ptr(), cols, w.data_ptr(), b.data_ptr(), y.data_ptr(), cols,
                                        rows, cols, eps, dtype_code(y.dtype), _stream(y)), "dp_layernorm")
 
 
 def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int = 16,
               head_dim: int = 64) -> None:
-    with _Timed("attention", 4.0 * batch * heads * seq * seq * head_dim):
+    with _Timed("attention", 4.0 * batch * heads * seq * seq * head_dim, (batch, seq)):
         check(_lib.load().dp_attention(qkv.data_ptr(), out.data_ptr(), batch, seq, heads, head_dim,
                                        head_dim ** -0.5, dtype_code(out.dtype), _stream(out)), "dp_attention")
 

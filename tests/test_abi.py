@@ -15,7 +15,7 @@ HEADER = os.path.join(REPO, "include", "dp_mi355x.h")
 
 def declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^int (dp_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t) (dp_\w+)\(", src, flags=re.M)))
 
 
 def test_header_and_python_export_lists_agree():
@@ -58,3 +58,30 @@ def test_argument_errors_are_reported_before_launch():
     assert lib.dp_attention(16, 16, 1, 577, 16, 128, 0.1, 0, None) == 1001
     with pytest.raises(_lib.DPError, match="DP_ERR_SHAPE"):
         _lib.check(1001, "x")
+
+
+def test_gemm_plan_tile_choice():
+    """dp_gemm_plan (host-only): engine choice for the frame's GEMM shapes (tile, workgroups)."""
+    lib = _lib.load()
+    t, g = ctypes.c_int32(), ctypes.c_int32()
+
+    def plan(M, N, K, **kw):
+        a = _lib.GemmArgs()
+        a.M, a.N, a.K = M, N, K
+        a.A = a.B = a.C = 256
+        a.lda, a.ldb, a.ldc = K, K, N
+        for k, v in kw.items():
+            setattr(a, k, v)
+        rc = lib.dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g))
+        return rc, t.value, g.value
+
+    # ViT-L patch encoder (M = 35 x 577 = 20195 = 64 tiles of 320 rows)
+    assert plan(20195, 3072, 1024)[1:] == (_lib.DP_TILE_BIG_320x256, 64 * 12)
+    assert plan(20195, 1024, 1024)[1:] == (_lib.DP_TILE_BIG_320x256, 64 * 4)     # one round on 256 CUs
+    assert plan(20195, 4096, 1024)[1:] == (_lib.DP_TILE_8PH_256x256, 79 * 16)
+    assert plan(577, 3072, 1024)[1:] == (_lib.DP_TILE_BIG_256x128, 3 * 24)       # side encoders
+    # stream-K is opt-in and needs a workspace
+    assert plan(20195, 3072, 1024, tile=_lib.DP_TILE_STREAMK_256x256)[0] == 1000
+    ws = lib.dp_gemm_workspace_size()
+    rc, tile, wgs = plan(20195, 3072, 1024, tile=_lib.DP_TILE_STREAMK_256x256, workspace=256, workspace_bytes=ws)
+    assert rc == 0 and tile == _lib.DP_TILE_STREAMK_256x256 and 1 <= wgs <= 256

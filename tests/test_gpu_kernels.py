@@ -13,7 +13,8 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 from depth_pro import ops  # noqa: E402
-from depth_pro._lib import DP_ACT_GELU, DP_ACT_RELU  # noqa: E402
+from depth_pro._lib import (DP_ACT_GELU, DP_ACT_RELU, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa: E402
+                            DP_TILE_BIG_256x256, DP_TILE_BIG_320x256, DP_TILE_STREAMK_256x256)
 
 DTYPES = [torch.bfloat16, torch.float16]
 
@@ -254,3 +255,95 @@ def test_gemm_every_tile_engine(cuda, tile):
              relu_a=True, tile=TILES[tile])
     ref = F.conv2d(F.relu(x.float()), w.float(), padding=1)
     close(out.reshape(1, S, S, cout).permute(0, 3, 1, 2), ref, dt, f"conv {tile}")
+
+
+# ------------------------------------------------------------ stream-K engine
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,N,K,mode", [
+    (20195, 3072, 1024, "bias"),          # qkv: 948 tiles over 256 persistent workgroups (split tiles)
+    (20195, 1024, 1024, "acc"),           # proj: fp32 residual accumulate + LayerScale
+    (5000, 1024, 4096, "acc"),            # fc2-like, long K
+    (20195, 4096, 1024, "gelu"),          # fc1
+    (300, 256, 64, "bias"),               # 2 tiles, 1 k-step
+    (4100, 512, 192, "bias"),             # 34 tiles x 3 k-steps, ragged last m-tile
+])
+def test_gemm_stream_k_matches_reference_and_data_parallel(cuda, dt, M, N, K, mode):
+    g = torch.Generator().manual_seed(M + 7 * N + K)
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    gamma = torch.rand(N, generator=g).to(cuda)
+    ws = ops.gemm_workspace(cuda)
+    kw = dict(M=M, N=N, K=K, bias=bias)
+    ref = A.float() @ B.float().t() + bias
+    if mode == "acc":
+        X = torch.randn(M, N, generator=g).to(cuda)
+        kw.update(gamma=gamma, accumulate=True)
+        C1, C2 = X.clone(), X.clone()
+        ref = X + gamma * ref
+    else:
+        if mode == "gelu":
+            kw.update(act=DP_ACT_GELU)
+            ref = F.gelu(ref)
+        C1 = torch.empty(M, N, dtype=dt, device=cuda)
+        C2 = torch.empty(M, N, dtype=dt, device=cuda)
+    ops.gemm(A, B, C1, tile=DP_TILE_STREAMK_256x256, workspace=ws, **kw)
+    ops.gemm(A, B, C2, tile=DP_TILE_BIG_256x256, **kw)
+    torch.cuda.synchronize()
+    assert int(ws[4092:4096].view(torch.int32).item()) == 0, "stream-K partial wait timed out"
+    close(C1, ref, torch.float32 if (mode == "acc" and dt == torch.float16) else dt, "stream-K")
+    # same tiles, same k order except where a tile's k range was split: fp32 sums agree to rounding
+    d = (C1.float() - C2.float()).abs().max().item()
+    assert d <= 1e-2 * (C2.float().abs().max().item() + 1e-6), d
+    # deterministic: a second run is bit-identical
+    C3 = X.clone() if mode == "acc" else torch.empty_like(C1)
+    ops.gemm(A, B, C3, tile=DP_TILE_STREAMK_256x256, workspace=ws, **kw)
+    assert torch.equal(C1, C3)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_stream_k_conv3x3_relu_residual(cuda, dt):
+    """Implicit-GEMM 3x3 conv (decoder ResidualBlock shape) through the stream-K engine."""
+    g = torch.Generator().manual_seed(11)
+    S, C = 96, 256
+    x = rnd(1, C, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(C, C, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * C) ** -0.5)
+    b = torch.randn(C, generator=g).to(cuda)
+    r = rnd(1, C, S, S, dt=dt, dev=cuda, gen=g)
+    xh = x.permute(0, 2, 3, 1).reshape(S * S, C).contiguous()
+    rh = r.permute(0, 2, 3, 1).reshape(S * S, C).contiguous()
+    wp = w.permute(0, 2, 3, 1).reshape(C, 9 * C).contiguous()
+    out = torch.empty(S * S, C, dtype=dt, device=cuda)
+    ops.gemm(xh, wp, out, M=S * S, N=C, K=9 * C, conv=dict(in_h=S, in_w=S, in_c=C, k=3, stride=1, pad=1,
+                                                            out_h=S, out_w=S),
+             relu_a=True, bias=b, R1=rh, ldr1=C, tile=DP_TILE_STREAMK_256x256, workspace=ops.gemm_workspace(cuda))
+    ref = F.conv2d(F.relu(x.float()), w.float(), b, padding=1) + r.float()
+    close(out.reshape(1, S, S, C).permute(0, 3, 1, 2), ref, dt, "stream-K conv3x3")
+
+
+ENGINES = [DP_TILE_BIG_256x256, DP_TILE_8PH_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_256x128, DP_TILE_STREAMK_256x256]
+
+
+@pytest.mark.parametrize("tile", ENGINES)
+@pytest.mark.parametrize("dt", DTYPES)
+def test_every_big_engine_on_ragged_conv_and_dense(cuda, dt, tile):
+    """Each tile engine on a ragged-M dense GEMM (bias + GELU) and a strided 3x3 conv with ReLU-on-load."""
+    g = torch.Generator().manual_seed(tile)
+    ws = ops.gemm_workspace(cuda)
+    M, N, K = 1337, 512, 320
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    C = torch.empty(M, N, dtype=dt, device=cuda)
+    ops.gemm(A, B, C, M=M, N=N, K=K, bias=bias, act=DP_ACT_GELU, tile=tile, workspace=ws)
+    close(C, F.gelu(A.float() @ B.float().t() + bias), dt, f"dense tile {tile}")
+    S, Ci, Co = 50, 128, 256
+    x = rnd(1, Ci, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(Co, Ci, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * Ci) ** -0.5)
+    So = (S + 2 - 3) // 2 + 1
+    out = torch.empty(So * So, Co, dtype=dt, device=cuda)
+    ops.gemm(x.permute(0, 2, 3, 1).reshape(S * S, Ci).contiguous(), w.permute(0, 2, 3, 1).reshape(Co, -1).contiguous(),
+             out, M=So * So, N=Co, K=9 * Ci, conv=dict(in_h=S, in_w=S, in_c=Ci, k=3, stride=2, pad=1, out_h=So, out_w=So),
+             relu_a=True, tile=tile, workspace=ws)
+    ref = F.conv2d(F.relu(x.float()), w.float(), stride=2, padding=1)
+    close(out.reshape(1, So, So, Co).permute(0, 3, 1, 2), ref, dt, f"conv tile {tile}")

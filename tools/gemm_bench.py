@@ -8,7 +8,16 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
 from depth_pro import ops  # noqa: E402
 from depth_pro._lib import (DP_TILE_128x128, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa
-                            DP_TILE_BIG_256x128_K32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32)
+                            DP_TILE_BIG_256x128_K32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32,
+                            DP_TILE_DEEP4_256x256, DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128,
+                            DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256)
+
+TILES = (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
+         ("8ph256x256", DP_TILE_8PH_256x256), ("deep4_256x256", DP_TILE_DEEP4_256x256),
+         ("deep5_256x256", DP_TILE_DEEP5_256x256), ("deep6_256x128", DP_TILE_DEEP_256x128),
+         ("sk256x256", DP_TILE_STREAMK_256x256), ("big320x256", DP_TILE_BIG_320x256))
+N256 = (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
+        DP_TILE_DEEP5_256x256, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256)
 
 SHAPES = [  # (name, M, N, K, kw)
     ("qkv", 20195, 3072, 1024, {}),
@@ -41,11 +50,13 @@ def main():
     ap.add_argument("--only", default=None, help="substring of one shape name")
     ap.add_argument("--tile", default=None, help="128x128 | big256x256 | big256x128")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--torch-only", action="store_true", help="time only torch.matmul (hipBLASLt) on the dense shapes")
     ap.add_argument("--ablate", action="store_true", help="time the no-store / no-load / no-mfma variants")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
+    ws = ops.gemm_workspace(dev)
     for name, M, N, K, kw in SHAPES:
         if args.only and args.only not in name:
             continue
@@ -62,14 +73,13 @@ def main():
         C = torch.zeros(M, N, device=dev, dtype=torch.float32 if kw.get("acc") else dt)
         flop = 2.0 * M * N * K
         res = []
-        for tname, tile in (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
-                            ("8ph256x256", DP_TILE_8PH_256x256)):
-            if tile in (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256) and N % 256:
+        for tname, tile in (() if args.torch_only else TILES):
+            if tile in N256 and N % 256:
                 continue
-            if args.tile and args.tile != tname:
+            if args.tile and tname not in args.tile.split(","):
                 continue
             f = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, conv=conv, bias=bias, act=2 if kw.get("gelu") else 0,
-                                 accumulate=bool(kw.get("acc")), tile=tile)  # noqa: E731
+                                 accumulate=bool(kw.get("acc")), tile=tile, workspace=ws)  # noqa: E731
             ms = timeit(f, args.iters)
             res.append(f"{tname} {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
             if args.ablate and tname.startswith("big"):
@@ -81,18 +91,18 @@ def main():
                 _lib.load().dp_gemm_debug_flags(0)
                 res.append("[" + " ".join(parts) + "]")
         # correctness of the big engine vs the small one on this shape
-        if not kw.get("acc") and not args.tile:
+        if not kw.get("acc") and not args.tile and not args.torch_only:
             C1 = torch.empty_like(C)
             ops.gemm(A, B, C1, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_128x128)
             C2 = torch.empty_like(C)
             d = 0.0
-            for t in (DP_TILE_BIG_256x128, DP_TILE_8PH_256x256):
-                if t == DP_TILE_8PH_256x256 and N % 256:
+            for _, t in TILES:
+                if t in N256 and N % 256:
                     continue
-                ops.gemm(A, B, C2, M=M, N=N, K=K, conv=conv, bias=bias, tile=t)
+                ops.gemm(A, B, C2, M=M, N=N, K=K, conv=conv, bias=bias, tile=t, workspace=ws)
                 d = max(d, (C1.float() - C2.float()).abs().max().item())
             res.append(f"max|small-big|={d:.2e}")
-        if conv is None and not args.tile:
+        if conv is None and (not args.tile or args.torch_only):
             ms = timeit(lambda: torch.matmul(A, B.t()))
             res.append(f"torch.matmul {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
         print(f"{name:28s} " + " | ".join(res), flush=True)
