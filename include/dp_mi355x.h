@@ -34,10 +34,10 @@ enum { DP_BF16 = 0, DP_F16 = 1, DP_F32 = 2 };
 enum { DP_OK = 0, DP_ERR_ARG = 1000, DP_ERR_SHAPE = 1001, DP_ERR_ALIGN = 1002, DP_ERR_DTYPE = 1003 };
 enum { DP_ACT_NONE = 0, DP_ACT_RELU = 1, DP_ACT_GELU = 2 };
 enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
-enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1 };
+enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 2
+#define DP_ABI_VERSION 3
 int dp_abi_version(void);
 
 /*
@@ -68,6 +68,13 @@ int dp_abi_version(void);
  *                                address C + pixel*ldc + co.
  * Fused 1x1 head (head_w != NULL; requires N <= 32): out[m] = relu(sum_n v[n]*head_w[n] + head_b)
  *   written as fp32 to C[m] (the depth head tail, depth_pro.py:200-204).
+ * DP_STORE_HEAD_PS (depth head deconv + conv3x3 + ReLU + 1x1 + ReLU, depth_pro.py:182-207, composed
+ *   at pack time into ONE 3x3 implicit conv over the pre-upsampling map): A_CONV over [out_h][out_w]
+ *   pixels, N = 128 columns = (parity q = 2*dy+dx, channel o < 32); per output pixel
+ *   (2y+dy, 2x+dx) of the 2*out_h x 2*out_w fp32 map C:
+ *   relu(sum_o head_w[o] * relu(v[q*32+o] - border(q, y, x, o)) + head_b), where border() sums
+ *   head_corr[(a*3+c)*32 + o] over the taps (a, c) of the 3x3 kernel that fall outside the
+ *   upsampled image (the deconv bias those zero-padded taps must not carry).
  */
 typedef struct dp_gemm_args {
   int32_t M, N, K;
@@ -98,6 +105,7 @@ typedef struct dp_gemm_args {
   int32_t row_group, row_group_out, row_off;
   const float* head_w;      /* [N] or NULL */
   float head_b;
+  const float* head_corr;   /* DP_STORE_HEAD_PS: [9][32] border corrections, else NULL */
   int32_t tile;             /* 0 = auto, else a DP_TILE_* hint */
   void* workspace;          /* NULL, or >= dp_gemm_workspace_size() bytes of device memory owned by
                                the caller for THIS stream (never shared by concurrent launches);

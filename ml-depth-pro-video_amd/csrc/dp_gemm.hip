@@ -53,6 +53,7 @@ struct GemmP {
   int row_group, row_group_out, row_off;
   const float* head_w;
   float head_b;
+  const float* head_corr;
   int tiles_n, tiles_m;
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
 };
@@ -362,6 +363,56 @@ __device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc
       o.z = (uint32_t)K_::from_f(x[4]) | ((uint32_t)K_::from_f(x[5]) << 16);
       o.w = (uint32_t)K_::from_f(x[6]) | ((uint32_t)K_::from_f(x[7]) << 16);
       *(uint4*)((u16*)p.C + off[it]) = o;
+    }
+  }
+}
+
+// DP_STORE_HEAD_PS epilogue (depth head tail, depth_pro.py:182-207, composed at
+// pack time): the GEMM ran the 3x3 conv of head.2 over the 2x-upsampled map as a
+// 3x3 conv of the pre-upsampling map h0 whose N = 128 columns are (parity q =
+// 2*dy + dx, channel o < 32).  Per output pixel (2y+dy, 2x+dx): z = acc + bias,
+// minus the deconv-bias share of the taps that fall in head.2's zero padding
+// (image border only), ReLU, dot with head.4's 32 weights, + bias, ReLU -> fp32.
+// The 8 columns of a lane lie in one parity group; the 4 lanes of a row finish
+// the 32-channel dot with two xor-shuffles.  Requires TN == 32 (one parity per wave).
+template <int NIT>
+__device__ __forceinline__ void head_ps_rows(const GemmP& p, const ColConst& cc, const int (&ms)[NIT], int n,
+                                             float (&v)[NIT][8], int lane) {
+  const int q = n >> 5, o0 = n & 31, dy = q >> 1, dx = q & 1;
+  const int hw = p.out_h * p.out_w;
+  float hw8[8];
+  #pragma unroll
+  for (int r = 0; r < 8; ++r) hw8[r] = p.head_w[o0 + r];
+  #pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int m = ms[it] < p.M ? ms[it] : p.M - 1;
+    const int b = m / hw, rr = m - b * hw;
+    const int y = rr / p.out_w, x = rr - y * p.out_w;
+    float z[8];
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) z[r] = v[it][r] + cc.b[r];
+    const bool top = y == 0 && dy == 0, bot = y == p.out_h - 1 && dy == 1;
+    const bool lft = x == 0 && dx == 0, rgt = x == p.out_w - 1 && dx == 1;
+    if (top || bot || lft || rgt) {
+      #pragma unroll
+      for (int a = 0; a < 3; ++a)
+        #pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const bool oob = (a == 0 && top) || (a == 2 && bot) || (c == 0 && lft) || (c == 2 && rgt);
+          if (oob) {
+            #pragma unroll
+            for (int r = 0; r < 8; ++r) z[r] -= p.head_corr[(a * 3 + c) * 32 + o0 + r];
+          }
+        }
+    }
+    float hs = 0.f;
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) hs += fmaxf(z[r], 0.f) * hw8[r];
+    hs += __shfl_xor(hs, 1);
+    hs += __shfl_xor(hs, 2);
+    if ((lane & 3) == 0 && ms[it] < p.M) {
+      const long long W2 = 2LL * p.out_w;
+      ((float*)p.C)[((long long)b * 2 * p.out_h + 2 * y + dy) * W2 + 2 * x + dx] = fmaxf(hs + p.head_b, 0.f);
     }
   }
 }
@@ -706,6 +757,12 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       #pragma unroll
       for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
       ms[it] = m0 + wm * TM + q * 32 + row;
+    }
+    if constexpr (TN == 32) {
+      if (p.store_mode == DP_STORE_HEAD_PS) {
+        head_ps_rows<NIT>(p, cc, ms, n_l, v, lane);
+        continue;
+      }
     }
     epilogue_rows<K_, NIT>(p, cc, ms, n_l, v);
   }
@@ -1429,6 +1486,11 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     if (a->out_h <= 0 || a->out_w <= 0 || a->stride <= 0 || a->M % (a->out_h * a->out_w) != 0)
       return DP_ERR_SHAPE;
   }
+  if (a->store_mode == DP_STORE_HEAD_PS) {
+    if (a->a_mode != DP_A_CONV || a->N != 128 || !a->head_w || !a->head_corr || a->c_dtype != DP_F32 ||
+        a->accumulate || a->R1 || a->R2 || a->pos || a->gamma || a->act != DP_ACT_NONE)
+      return DP_ERR_ARG;
+  }
   if (a->store_mode == DP_STORE_DECONV2X2) {
     if (a->dc_cout % 4 != 0 || a->N != 4 * a->dc_cout || a->dc_h <= 0 || a->dc_w <= 0 ||
         a->M % (a->dc_h * a->dc_w) != 0)
@@ -1436,7 +1498,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
   tile = a->tile;
-  if (a->head_w) {
+  if (a->store_mode == DP_STORE_HEAD_PS) {
+    tile = DP_TILE_BIG_256x128;   // TN = 32: one parity group per wave column
+  } else if (a->head_w) {
     if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;
     tile = DP_TILE_256x32;
   }
@@ -1478,7 +1542,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.C = a->C; p.ldc = a->ldc; p.c_dtype = a->c_dtype; p.accumulate = a->accumulate;
   p.store_mode = a->store_mode; p.dc_h = a->dc_h; p.dc_w = a->dc_w; p.dc_cout = a->dc_cout;
   p.row_group = a->row_group; p.row_group_out = a->row_group_out; p.row_off = a->row_off;
-  p.head_w = a->head_w; p.head_b = a->head_b;
+  p.head_w = a->head_w; p.head_b = a->head_b; p.head_corr = a->head_corr;
   p.tiles_n = 1;
   p.tiles_m = 1;
   if (tile == DP_TILE_STREAMK_256x256) {

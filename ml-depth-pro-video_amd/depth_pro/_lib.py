@@ -16,11 +16,11 @@ import torch  # noqa: F401  (loads the HIP runtime first; libdp links the same S
 DP_BF16, DP_F16, DP_F32 = 0, 1, 2
 DP_ACT_NONE, DP_ACT_RELU, DP_ACT_GELU = 0, 1, 2
 DP_A_DENSE, DP_A_CONV = 0, 1
-DP_STORE_ROWS, DP_STORE_DECONV2X2 = 0, 1
+DP_STORE_ROWS, DP_STORE_DECONV2X2, DP_STORE_HEAD_PS = 0, 1, 2
 (DP_TILE_AUTO, DP_TILE_128x128, DP_TILE_256x64, DP_TILE_256x32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x128,
  DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256) = range(14)
-DP_ABI_VERSION = 2
+DP_ABI_VERSION = 3
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -59,7 +59,7 @@ class GemmArgs(ctypes.Structure):
         ("store_mode", ctypes.c_int32),
         ("dc_h", ctypes.c_int32), ("dc_w", ctypes.c_int32), ("dc_cout", ctypes.c_int32),
         ("row_group", ctypes.c_int32), ("row_group_out", ctypes.c_int32), ("row_off", ctypes.c_int32),
-        ("head_w", ctypes.c_void_p), ("head_b", ctypes.c_float),
+        ("head_w", ctypes.c_void_p), ("head_b", ctypes.c_float), ("head_corr", ctypes.c_void_p),
         ("tile", ctypes.c_int32),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
     ]

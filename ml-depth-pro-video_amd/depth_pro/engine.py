@@ -53,6 +53,38 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
     return t.detach().to(torch.float32).contiguous()
 
 
+def compose_head(wd: torch.Tensor, bd: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, dt) -> Dict[str, object]:
+    """Compose the depth head's ConvTranspose2d(k2, s2) (head.1) with the 3x3 conv after it
+    (head.2) -- linear, nothing in between (depth_pro.py:182-207) -- into ONE 3x3 conv over
+    the pre-upsampling map whose 128 outputs are (parity q = 2*dy + dx, channel o):
+
+        W'[q, o, ty, tx, ci] = sum over taps (a, b) of head.2 that land in h0 pixel
+                               (y + ty - 1, x + tx - 1) of  W2[o, c, a, b] Wd[ci, c, py, px]
+
+    with (py, px) the deconv sub-pixel each tap reads.  The deconv bias rides along as a
+    per-column bias; `corr[a, b, o] = sum_c W2[o, c, a, b] bd[c]` is what a tap that falls
+    in head.2's zero padding must NOT contribute (subtracted at the image border).
+    Removes the 1536^2 x 128 intermediate (604 MB written + re-read 9x) from the frame.
+    """
+    ci_n, c_n = wd.shape[0], wd.shape[1]
+    o_n = w2.shape[0]
+    wc = torch.zeros(4, o_n, 3, 3, ci_n, dtype=torch.float32, device=wd.device)
+    for dy in range(2):
+        for dx in range(2):
+            q = 2 * dy + dx
+            for a in range(-1, 2):
+                ry = dy + a
+                ty, py = ry // 2 + 1, ry & 1
+                for b in range(-1, 2):
+                    rx = dx + b
+                    tx, px = rx // 2 + 1, rx & 1
+                    wc[q, :, ty, tx, :] += w2[:, :, a + 1, b + 1] @ wd[:, :, py, px].t()
+    corr = torch.einsum("ocab,c->abo", w2, bd).contiguous()             # [3, 3, o]
+    bias = (b2 + corr.sum(dim=(0, 1))).repeat(4).contiguous()           # interior: all 9 taps
+    return {"head.ps.w": wc.reshape(4 * o_n, 9 * ci_n).to(dt).contiguous(), "head.ps.b": bias,
+            "head.ps.corr": corr.reshape(-1).contiguous()}
+
+
 def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: int) -> Dict[str, object]:
     """Convert a (reference-named) state dict into GEMM-ready device tensors.
 
@@ -115,10 +147,8 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: 
     # head
     P["head.0.w"] = _conv_w(g("head.0.weight"), dt)
     P["head.0.b"] = _f32(g("head.0.bias"))
-    P["head.1.w"] = _deconv_w(g("head.1.weight"), dt)
-    P["head.1.b"] = _f32(g("head.1.bias")).repeat(4)
-    P["head.2.w"] = _conv_w(g("head.2.weight"), dt)
-    P["head.2.b"] = _f32(g("head.2.bias"))
+    P.update(compose_head(_f32(g("head.1.weight")), _f32(g("head.1.bias")), _f32(g("head.2.weight")),
+                          _f32(g("head.2.bias")), dt))
     P["head.4.w"] = _f32(g("head.4.weight")).reshape(-1)
     P["head.4.b"] = float(sd["head.4.bias"].detach().float().reshape(-1)[0])
     if "fov.encoder.1.weight" in sd:
@@ -200,7 +230,6 @@ class Engine:
         self.feats = e(768 * 768, 256)
         # head
         self.h0 = e(768 * 768, 128)
-        self.h1 = e(1536 * 1536, 128)
         self.canonical = e(1, 1, S, S, dtype=torch.float32)
         # fov
         self.fov_tok = e(PTOK, 128)
@@ -364,11 +393,12 @@ class Engine:
             feats = self.feats
         if "head" in _ABLATE:
             return self.canonical, self.fov_deg
-        # head (depth_pro.py:182-207): conv3x3 -> deconv -> conv3x3+ReLU -> 1x1+ReLU (fused)
+        # head (depth_pro.py:182-207): conv3x3, then deconv -> conv3x3 -> ReLU -> 1x1 -> ReLU as ONE
+        # composed 3x3 conv over h0 with a pixel-shuffle + fused 1x1 epilogue (compose_head)
         self._conv3(feats, 768, 256, P["head.0.w"], self.h0, 128, bias=P["head.0.b"])
-        self._deconv(self.h0, 768, 128, P["head.1.w"], self.h1, 128, bias=P["head.1.b"])
-        self._conv3(self.h1, 1536, 128, P["head.2.w"], self.canonical, 32, bias=P["head.2.b"], act=DP_ACT_RELU,
-                    head_w=P["head.4.w"], head_b=P["head.4.b"])
+        ops.gemm(self.h0, P["head.ps.w"], self.canonical, M=768 * 768, N=128, K=9 * 128,
+                 conv=dict(in_h=768, in_w=768, in_c=128, k=3, stride=1, pad=1, out_h=768, out_w=768),
+                 bias=P["head.ps.b"], head_w=P["head.4.w"], head_b=P["head.4.b"], head_corr=P["head.ps.corr"])
         return self.canonical, self.fov_deg
 
     # ---------------------------------------------------------------- graphs

@@ -14,7 +14,7 @@ import torch
 
 from . import _lib
 from ._lib import (DP_A_CONV, DP_A_DENSE, DP_ACT_NONE, DP_BF16, DP_F16, DP_F32,
-                   DP_STORE_DECONV2X2, DP_STORE_ROWS, GemmArgs, check)
+                   DP_STORE_DECONV2X2, DP_STORE_HEAD_PS, DP_STORE_ROWS, GemmArgs, check)
 
 _TORCH_DT = {DP_BF16: torch.bfloat16, DP_F16: torch.float16, DP_F32: torch.float32}
 
@@ -111,6 +111,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          accumulate: bool = False, deconv: Optional[tuple] = None,
          row_group: int = 0, row_group_out: int = 0, row_off: int = 0,
          head_w: Optional[torch.Tensor] = None, head_b: float = 0.0,
+         head_corr: Optional[torch.Tensor] = None,
          A_off: int = 0, C_off: int = 0, tile: int = 0, workspace: Optional[torch.Tensor] = None,
          plan_only: bool = False):
     """dp_gemm. `A_off`/`C_off` are element offsets into A / C (sub-views).
@@ -149,11 +150,14 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     if deconv is not None:
         a.store_mode = DP_STORE_DECONV2X2
         a.dc_h, a.dc_w, a.dc_cout = deconv
+    elif head_corr is not None:
+        a.store_mode = DP_STORE_HEAD_PS
     else:
         a.store_mode = DP_STORE_ROWS
     a.row_group, a.row_group_out, a.row_off = row_group, row_group_out, row_off
     a.head_w = _p(head_w)
     a.head_b = float(head_b)
+    a.head_corr = _p(head_corr)
     a.tile = tile
     ws = workspace if workspace is not None else _WS
     if ws is not None:

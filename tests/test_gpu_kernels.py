@@ -347,3 +347,27 @@ def test_every_big_engine_on_ragged_conv_and_dense(cuda, dt, tile):
              relu_a=True, tile=tile, workspace=ws)
     ref = F.conv2d(F.relu(x.float()), w.float(), stride=2, padding=1)
     close(out.reshape(1, So, So, Co).permute(0, 3, 1, 2), ref, dt, f"conv tile {tile}")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_head_pixel_shuffle_epilogue(cuda, dt):
+    """Composed depth head (deconv -> 3x3 -> ReLU -> 1x1 -> ReLU) as one HEAD_PS GEMM vs the layer order."""
+    from depth_pro.engine import compose_head
+
+    g = torch.Generator().manual_seed(21)
+    ci, H, W = 128, 40, 36
+    h0 = (torch.randn(1, ci, H, W, generator=g)).to(dt).float()
+    wd = torch.randn(ci, ci, 2, 2, generator=g) * ci ** -0.5
+    bd = torch.randn(ci, generator=g)
+    w2 = torch.randn(32, ci, 3, 3, generator=g) * (9 * ci) ** -0.5
+    b2 = torch.randn(32, generator=g)
+    w4 = torch.randn(32, generator=g) * 32 ** -0.5
+    P = {k: (v.to(cuda) if torch.is_tensor(v) else v) for k, v in compose_head(wd, bd, w2, b2, dt).items()}
+    out = torch.full((2 * H, 2 * W), float("nan"), device=cuda)
+    x = h0[0].permute(1, 2, 0).reshape(H * W, ci).contiguous().to(dt).to(cuda)
+    ops.gemm(x, P["head.ps.w"], out, M=H * W, N=128, K=9 * ci,
+             conv=dict(in_h=H, in_w=W, in_c=ci, k=3, stride=1, pad=1, out_h=H, out_w=W),
+             bias=P["head.ps.b"], head_w=w4.to(cuda), head_b=0.25, head_corr=P["head.ps.corr"])
+    ref = F.conv_transpose2d(h0, wd, bd, stride=2)
+    ref = F.relu(F.conv2d(F.relu(F.conv2d(ref, w2, b2, padding=1)), w4.reshape(1, 32, 1, 1), torch.tensor([0.25])))
+    close(out, ref[0, 0], dt, "head HEAD_PS")
