@@ -53,9 +53,11 @@ int dp_abi_version(void);
  * A operand: DP_A_DENSE  -> A[m][k] row-major, leading dim lda (elements);
  *            DP_A_CONV   -> implicit im2col of an NHWC tensor [batch][in_h][in_w][in_c]
  *                           for a k_h x k_w conv (stride, pad) with output out_h x out_w;
- *                           M = batch*out_h*out_w, K = k_h*k_w*in_c, k = (ky,kx,ci).
+ *                           M = batch*out_h*out_w, K = k_h*k_w*in_c,
+ *                           k = ((ci/64 * k_h + ky) * k_w + kx) * 64 + ci%64 (the taps of one
+ *                           64-channel block are consecutive: shifted input re-reads hit L2).
  * B operand: packed weights B[n][k] row-major (ldb), i.e. W for a Linear,
- *            [Cout][ky][kx][Cin] for a conv, [(dy,dx,Cout)][Cin] for a k2s2 deconv.
+ *            [Cout][Cin/64][ky][kx][64] for a conv, [(dy,dx,Cout)][Cin] for a k2s2 deconv.
  * Requirements: K % 64 == 0, N % 4 == 0, lda/ldb % 8 == 0, in_c % 64 == 0 (conv).
  *
  * Epilogue, per element, in this order:

@@ -33,7 +33,7 @@ struct GemmP {
   const u16* B;
   long long ldb;
   int relu_a;
-  int in_h, in_w, in_c, k_w, stride, pad, out_h, out_w;
+  int in_h, in_w, in_c, k_h, k_w, stride, pad, out_h, out_w;
   const float* bias;
   int act;
   const float* gamma;
@@ -440,6 +440,21 @@ __device__ __forceinline__ const u16* conv_src(const GemmP& p, const ConvRow& r,
   return p.A + pix * p.in_c + ci;
 }
 
+// Implicit-conv K order: k = ((cb * k_h + ky) * k_w + kx) * 64 + c -- the taps of one
+// 64-channel block are consecutive K steps, so the shifted re-reads of the same input
+// lines by neighbouring taps are one K step apart and hit in L2 (with the channel block
+// innermost, the re-read came 4-36 steps later, after the XCD's 32 workgroups had
+// streamed several MiB through the 4 MiB L2).  Weights are packed to match
+// ([Cout][Cin/64][ky][kx][64], ops.conv_weight).  k0 % 32 == 0.
+__device__ __forceinline__ void conv_tap(const GemmP& p, int k0, int& ky, int& kx, int& ci) {
+  const int chunk = k0 >> 6, c = k0 & 63;
+  const int taps = p.k_h * p.k_w;
+  const int cb = chunk / taps, tap = chunk - cb * taps;
+  ky = tap / p.k_w;
+  kx = tap - ky * p.k_w;
+  ci = cb * 64 + c;
+}
+
 // ============================================================ big-tile engine
 constexpr int NT_BIG = 512;
 
@@ -542,13 +557,13 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
     const int n = n0 + i * ROWS_PER_ROUND + prow;
     b_src[i] = p.B + (long long)(n < p.N ? n : p.N - 1) * p.ldb + pchunk * 8;
   }
-  int t_ky = 0, t_kx = 0, t_ci = 0;  // conv tap of the next K tile to issue (uniform)
-
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
   auto issue = [&](int kt, int stage) {
     const uint32_t sa = lds_base + stage * STAGE;
     const uint32_t sb = sa + A_BYTES;
     const int k0 = kt * BKT;
+    int t_ky = 0, t_kx = 0, t_ci = 0;
+    if constexpr (CONV) conv_tap(p, k0, t_ky, t_kx, t_ci);
     #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const void* src;
@@ -560,13 +575,6 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
         src = a_src[i] + k0;
       }
       glds16(src, sa + i * 8192);
-    }
-    if constexpr (CONV) {
-      t_ci += BKT;
-      if (t_ci == p.in_c) {
-        t_ci = 0;
-        if (++t_kx == p.k_w) { t_kx = 0; ++t_ky; }
-      }
     }
     #pragma unroll
     for (int i = 0; i < LB; ++i) glds16(b_src[i] + k0, sb + i * 8192);
@@ -822,10 +830,7 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
     const uint32_t dst = lds_base + (t & 1) * TILEB + h * HALF;
     int ci = 0, ky = 0, kx = 0;
     if constexpr (CONV) {
-      const int k0 = t * 64, tap = k0 / p.in_c;
-      ci = k0 - tap * p.in_c;
-      ky = tap / p.k_w;
-      kx = tap - ky * p.k_w;
+      conv_tap(p, t * 64, ky, kx, ci);
     }
     #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1064,10 +1069,7 @@ __global__ void __launch_bounds__(512, 1) gemm_sk_kernel(const GemmP p, const Sk
     const int k0 = ks * 64;
     int ky = 0, kx = 0, ci = 0;
     if constexpr (CONV) {
-      const int tap = k0 / p.in_c;
-      ci = k0 - tap * p.in_c;
-      ky = tap / p.k_w;
-      kx = tap - ky * p.k_w;
+      conv_tap(p, k0, ky, kx, ci);
     }
     #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1297,13 +1299,14 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
   }
 
   uint4 ra[CA], rb[CB];
-  int t_ky = 0, t_kx = 0, t_ci = 0;
 
   auto load_tile = [&](int k0) {
     if constexpr (!CONV) {
       #pragma unroll
       for (int i = 0; i < CA; ++i) ra[i] = *(const uint4*)(a_ptr[i] + k0);
     } else {
+      int t_ky, t_kx, t_ci;
+      conv_tap(p, k0, t_ky, t_kx, t_ci);
       #pragma unroll
       for (int i = 0; i < CA; ++i) {
         bool inb;
@@ -1311,11 +1314,6 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(const GemmP p) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (inb) v = *(const uint4*)s;
         ra[i] = v;
-      }
-      t_ci += BK;
-      if (t_ci == p.in_c) {
-        t_ci = 0;
-        if (++t_kx == p.k_w) { t_kx = 0; ++t_ky; }
       }
     }
     #pragma unroll
@@ -1534,7 +1532,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.A = (const u16*)a->A; p.lda = a->lda;
   p.B = (const u16*)a->B; p.ldb = a->ldb;
   p.relu_a = a->relu_a;
-  p.in_h = a->in_h; p.in_w = a->in_w; p.in_c = a->in_c; p.k_w = a->k_w;
+  p.in_h = a->in_h; p.in_w = a->in_w; p.in_c = a->in_c; p.k_h = a->k_h; p.k_w = a->k_w;
   p.stride = a->stride; p.pad = a->pad; p.out_h = a->out_h; p.out_w = a->out_w;
   p.bias = a->bias; p.act = a->act; p.gamma = a->gamma;
   p.pos = a->pos; p.ldpos = a->ldpos; p.pos_group = a->pos_group; p.pos_off = a->pos_off;

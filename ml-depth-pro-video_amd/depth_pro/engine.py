@@ -38,9 +38,8 @@ D = EMBED_DIM
 
 # --------------------------------------------------------------------- packing
 def _conv_w(w: torch.Tensor, dt) -> torch.Tensor:
-    """Conv2d [Cout, Cin, kh, kw] -> B[Cout][(ky, kx, ci)]."""
-    co = w.shape[0]
-    return w.permute(0, 2, 3, 1).reshape(co, -1).to(dt).contiguous()
+    """Conv2d [Cout, Cin, kh, kw] -> B[Cout][(ci/64, ky, kx, ci%64)] (ops.conv_weight)."""
+    return ops.conv_weight(w, dt)
 
 
 def _deconv_w(w: torch.Tensor, dt) -> torch.Tensor:
@@ -81,7 +80,8 @@ def compose_head(wd: torch.Tensor, bd: torch.Tensor, w2: torch.Tensor, b2: torch
                     wc[q, :, ty, tx, :] += w2[:, :, a + 1, b + 1] @ wd[:, :, py, px].t()
     corr = torch.einsum("ocab,c->abo", w2, bd).contiguous()             # [3, 3, o]
     bias = (b2 + corr.sum(dim=(0, 1))).repeat(4).contiguous()           # interior: all 9 taps
-    return {"head.ps.w": wc.reshape(4 * o_n, 9 * ci_n).to(dt).contiguous(), "head.ps.b": bias,
+    w_conv = wc.reshape(4 * o_n, 3, 3, ci_n).permute(0, 3, 1, 2)            # as a Conv2d weight [(q,o), ci, ty, tx]
+    return {"head.ps.w": ops.conv_weight(w_conv, dt), "head.ps.b": bias,
             "head.ps.corr": corr.reshape(-1).contiguous()}
 
 

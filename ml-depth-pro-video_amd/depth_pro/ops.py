@@ -92,6 +92,19 @@ def gemm_workspace(device: torch.device) -> torch.Tensor:
     return torch.zeros(int(_lib.load().dp_gemm_workspace_size()), dtype=torch.uint8, device=device)
 
 
+def conv_weight(w: torch.Tensor, dt: Optional[torch.dtype] = None) -> torch.Tensor:
+    """Conv2d weight [Cout][Cin][kh][kw] -> dp_gemm implicit-conv B operand [Cout][Cin/64][kh][kw][64].
+
+    The K order puts the taps of one 64-channel block next to each other (see conv_tap in
+    dp_gemm.hip: neighbouring taps re-read the same input lines one K step apart, in L2).
+    """
+    co, ci, kh, kw = w.shape
+    if ci % 64:
+        raise _lib.DPError(f"conv input channels must be a multiple of 64, got {ci}")
+    b = w.reshape(co, ci // 64, 64, kh, kw).permute(0, 1, 3, 4, 2).reshape(co, -1)
+    return (b if dt is None else b.to(dt)).contiguous()
+
+
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 

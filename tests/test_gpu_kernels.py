@@ -94,7 +94,7 @@ def test_conv3x3_implicit_gemm(cuda, dt, S, cin, cout, stride):
     r1 = rnd(1, cout, (S + 2 - 3) // stride + 1, (S + 2 - 3) // stride + 1, dt=dt, dev=cuda, gen=g)
     so = (S + 2 - 3) // stride + 1
     xh = x.permute(0, 2, 3, 1).contiguous()
-    wp = w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous()
+    wp = ops.conv_weight(w)
     r1h = r1.permute(0, 2, 3, 1).contiguous()
     out = torch.empty(so * so, cout, dtype=dt, device=cuda)
     ops.gemm(xh, wp, out, M=so * so, N=cout, K=9 * cin,
@@ -130,7 +130,7 @@ def test_head_conv_with_fused_1x1(cuda, dt):
     b = torch.randn(32, generator=g).to(cuda)
     w4 = torch.rand(32, generator=g).to(cuda)
     out = torch.empty(S * S, dtype=torch.float32, device=cuda)
-    ops.gemm(x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).reshape(32, -1).contiguous(), out,
+    ops.gemm(x.permute(0, 2, 3, 1).contiguous(), ops.conv_weight(w), out,
              M=S * S, N=32, K=9 * cin, conv=dict(in_h=S, in_w=S, in_c=cin, k=3, stride=1, pad=1, out_h=S, out_w=S),
              bias=b, act=DP_ACT_RELU, head_w=w4, head_b=0.25)
     h = F.relu(F.conv2d(x.float(), w.float(), b, padding=1))
@@ -250,7 +250,7 @@ def test_gemm_every_tile_engine(cuda, tile):
     x = rnd(1, cin, S, S, dt=dt, dev=cuda, gen=g)
     w = rnd(cout, cin, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * cin) ** -0.5)
     out = torch.empty(S * S, cout, dtype=dt, device=cuda)
-    ops.gemm(x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).reshape(cout, -1).contiguous(), out,
+    ops.gemm(x.permute(0, 2, 3, 1).contiguous(), ops.conv_weight(w), out,
              M=S * S, N=cout, K=9 * cin, conv=dict(in_h=S, in_w=S, in_c=cin, k=3, stride=1, pad=1, out_h=S, out_w=S),
              relu_a=True, tile=TILES[tile])
     ref = F.conv2d(F.relu(x.float()), w.float(), padding=1)
@@ -312,7 +312,7 @@ def test_gemm_stream_k_conv3x3_relu_residual(cuda, dt):
     r = rnd(1, C, S, S, dt=dt, dev=cuda, gen=g)
     xh = x.permute(0, 2, 3, 1).reshape(S * S, C).contiguous()
     rh = r.permute(0, 2, 3, 1).reshape(S * S, C).contiguous()
-    wp = w.permute(0, 2, 3, 1).reshape(C, 9 * C).contiguous()
+    wp = ops.conv_weight(w)
     out = torch.empty(S * S, C, dtype=dt, device=cuda)
     ops.gemm(xh, wp, out, M=S * S, N=C, K=9 * C, conv=dict(in_h=S, in_w=S, in_c=C, k=3, stride=1, pad=1,
                                                             out_h=S, out_w=S),
@@ -342,7 +342,7 @@ def test_every_big_engine_on_ragged_conv_and_dense(cuda, dt, tile):
     w = rnd(Co, Ci, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * Ci) ** -0.5)
     So = (S + 2 - 3) // 2 + 1
     out = torch.empty(So * So, Co, dtype=dt, device=cuda)
-    ops.gemm(x.permute(0, 2, 3, 1).reshape(S * S, Ci).contiguous(), w.permute(0, 2, 3, 1).reshape(Co, -1).contiguous(),
+    ops.gemm(x.permute(0, 2, 3, 1).reshape(S * S, Ci).contiguous(), ops.conv_weight(w),
              out, M=So * So, N=Co, K=9 * Ci, conv=dict(in_h=S, in_w=S, in_c=Ci, k=3, stride=2, pad=1, out_h=So, out_w=So),
              relu_a=True, tile=tile, workspace=ws)
     ref = F.conv2d(F.relu(x.float()), w.float(), stride=2, padding=1)

@@ -17,8 +17,10 @@ pytestmark = pytest.mark.gpu
 # BASELINE.json target: depth L1 vs reference < 1e-3 (relative).  bf16 carries
 # 8 mantissa bits through 3 x 24 ViT-L blocks; the measured values are printed
 # and bounded here (see DESIGN.md "Parity").
-TOL = {torch.bfloat16: dict(canon=2e-2, depth=2e-2, fov=2e-3, fpx=5e-3),
-       torch.float16: dict(canon=5e-3, depth=5e-3, fov=5e-4, fpx=1e-3)}
+# Measured (round 1): bf16 canonical 2.0e-3 / depth 1.4e-3, f16 2.6e-4 / 1.7e-4 -- bounds at ~2x.
+# The f16 mode meets BASELINE's < 1e-3 depth L1; bf16 does not (8 mantissa bits).
+TOL = {torch.bfloat16: dict(canon=4e-3, depth=3e-3, fov=1e-3, fpx=2e-3),
+       torch.float16: dict(canon=6e-4, depth=5e-4, fov=3e-4, fpx=5e-4)}
 
 
 def frame(seed, h=1536, w=1536):

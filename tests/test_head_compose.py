@@ -15,7 +15,7 @@ from depth_pro.engine import compose_head
 def composed_head(h0, P, w4, b4):
     """What the HEAD_PS GEMM computes, evaluated with torch ops (fp32)."""
     n, ci, H, W = h0.shape
-    wc = P["head.ps.w"].float().reshape(128, 3, 3, ci).permute(0, 3, 1, 2)   # [(q,o), ci, ty, tx]
+    wc = P["head.ps.w"].float().reshape(128, ci // 64, 3, 3, 64).permute(0, 1, 4, 2, 3).reshape(128, ci, 3, 3)
     v = F.conv2d(h0, wc, padding=1) + P["head.ps.b"].reshape(1, 128, 1, 1)  # [n, (q,o), H, W]
     corr = P["head.ps.corr"].reshape(3, 3, 32)
     out = torch.empty(n, 1, 2 * H, 2 * W)

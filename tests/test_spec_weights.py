@@ -51,8 +51,12 @@ def test_conv_pack_layout_is_implicit_gemm_order():
     x = torch.randn(1, 64, 5, 5, generator=g, dtype=torch.float64)
     w = torch.randn(32, 64, 3, 3, generator=g, dtype=torch.float64)
     ref = F.conv2d(x, w, padding=1)
-    B = _conv_w(w, torch.float64)  # [co][(ky,kx,ci)]
-    xp = F.pad(x, (1, 1, 1, 1))[0].permute(1, 2, 0)  # (7,7,64) NHWC padded
-    cols = torch.stack([xp[y:y + 3, xx:xx + 3, :].reshape(-1) for y in range(5) for xx in range(5)])
+    x = torch.cat([x, torch.randn(1, 64, 5, 5, generator=g, dtype=torch.float64)], 1)   # 128 channels
+    w = torch.randn(32, 128, 3, 3, generator=g, dtype=torch.float64)
+    ref = F.conv2d(x, w, padding=1)
+    B = _conv_w(w, torch.float64)  # [co][(ci/64, ky, kx, ci%64)]
+    xp = F.pad(x, (1, 1, 1, 1))[0].permute(1, 2, 0)  # (7,7,128) NHWC padded
+    cols = torch.stack([xp[y:y + 3, xx:xx + 3, :].reshape(3, 3, 2, 64).permute(2, 0, 1, 3).reshape(-1)
+                        for y in range(5) for xx in range(5)])
     got = (cols @ B.t()).t().reshape(32, 5, 5)
     assert (got - ref[0]).abs().max() < 1e-10
