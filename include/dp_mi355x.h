@@ -212,6 +212,21 @@ int dp_infer_epilogue(const float* canonical, int32_t src_h, int32_t src_w, cons
                       int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
                       float* f_px_out, dp_stream_t stream);
 
+/*
+ * dp_depth_to_points: camera-space point cloud of a depth map -- the reference's
+ * depth_to_3d (img_to_normalized_pointcloud.py:819-856), used before its PLY write-out
+ * (:1318).  valid = !isnan(depth) && depth > 0, points in row-major pixel order (numpy
+ * boolean indexing), fp64 as numpy computes them:
+ *   x = -1*(u - W/2)*z/f, y = -1*(v - H/2)*z/f, z = depth      (f = f_px if use_given,
+ *   else (double)*f_px_dev, e.g. dp_infer_epilogue's f_px_out).
+ * row_offsets: int32 [H+1] scratch; receives the exclusive prefix of valid counts per row
+ * and the total in row_offsets[H].  xyz: fp64 [H*W][3] (capacity); rgb_out (optional):
+ * uint8 [H*W][3] colours gathered from rgb_hwc (uint8 [H][W][3]) at the same pixels.
+ */
+int dp_depth_to_points(const float* depth, int32_t H, int32_t W, const float* f_px_dev, double f_px,
+                       int32_t use_given, const uint8_t* rgb_hwc, int32_t* row_offsets, double* xyz,
+                       uint8_t* rgb_out, dp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -391,3 +391,108 @@ extern "C" int dp_infer_epilogue(const float* canonical, int32_t SH, int32_t SW,
   DP_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------- point cloud
+// depth_to_3d (reference img_to_normalized_pointcloud.py:819-856) with the row-major
+// compaction of numpy boolean indexing: valid = !isnan(d) && d > 0;
+//   x = -1 * (u - W/2) * z / f,  y = -1 * (v - H/2) * z / f,  z = d      (fp64, numpy's order)
+// Three launches: per-row valid counts, one exclusive scan over rows, per-row scatter
+// (a block-level prefix over each 256-pixel chunk keeps the reference point order).
+namespace {
+
+__device__ __forceinline__ bool depth_valid(float d) { return !(d != d) && d > 0.f; }
+
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* sh, int& total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < NT; o <<= 1) {
+    const int a = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += a;
+    __syncthreads();
+  }
+  total = sh[NT - 1];
+  const int ex = sh[t] - v;
+  __syncthreads();
+  return ex;
+}
+
+__global__ void __launch_bounds__(256) pts_count_kernel(const float* __restrict__ depth, int W, int* __restrict__ rows) {
+  __shared__ int sh[256];
+  const int y = blockIdx.x;
+  int c = 0;
+  for (int x = threadIdx.x; x < W; x += 256) c += depth_valid(depth[(long long)y * W + x]);
+  int total;
+  block_excl_scan<256>(c, sh, total);
+  if (threadIdx.x == 0) rows[y] = total;
+}
+
+__global__ void __launch_bounds__(1024) pts_scan_kernel(int* __restrict__ rows, int H) {
+  __shared__ int sh[1024];
+  int carry = 0;
+  for (int base = 0; base < H; base += 1024) {
+    const int i = base + threadIdx.x;
+    const int v = i < H ? rows[i] : 0;
+    int total;
+    const int ex = block_excl_scan<1024>(v, sh, total);
+    if (i < H) rows[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) rows[H] = carry;
+}
+
+__global__ void __launch_bounds__(256) pts_scatter_kernel(const float* __restrict__ depth, int H, int W,
+                                                          const float* __restrict__ f_dev, double f_host, int use_host,
+                                                          const uint8_t* __restrict__ rgb, const int* __restrict__ rows,
+                                                          double* __restrict__ xyz, uint8_t* __restrict__ rgb_out) {
+  __shared__ int sh[256];
+  const int y = blockIdx.x;
+  const double f = use_host ? f_host : (double)*f_dev;
+  const double cx = W / 2.0, cy = H / 2.0;
+  int off = rows[y];
+  for (int x0 = 0; x0 < W; x0 += 256) {
+    const int x = x0 + threadIdx.x;
+    const float d = x < W ? depth[(long long)y * W + x] : 0.f;
+    const int ok = x < W && depth_valid(d);
+    int total;
+    const int ex = block_excl_scan<256>(ok, sh, total);
+    if (ok) {
+      const long long i = off + ex;
+      const double z = (double)d;
+      double px = -1.0 * ((double)x - cx);
+      px = px * z;
+      px = px / f;
+      double py = -1.0 * ((double)y - cy);
+      py = py * z;
+      py = py / f;
+      xyz[3 * i] = px;
+      xyz[3 * i + 1] = py;
+      xyz[3 * i + 2] = z;
+      if (rgb_out) {
+        const uint8_t* s = rgb + ((long long)y * W + x) * 3;
+        rgb_out[3 * i] = s[0];
+        rgb_out[3 * i + 1] = s[1];
+        rgb_out[3 * i + 2] = s[2];
+      }
+    }
+    off += total;
+  }
+}
+
+}  // namespace
+
+extern "C" int dp_depth_to_points(const float* depth, int32_t H, int32_t W, const float* f_px_dev, double f_px,
+                                  int32_t use_given, const uint8_t* rgb_hwc, int32_t* row_offsets, double* xyz,
+                                  uint8_t* rgb_out, dp_stream_t stream) {
+  if (!depth || !row_offsets || !xyz || (!use_given && !f_px_dev) || (rgb_out && !rgb_hwc)) return DP_ERR_ARG;
+  if (H <= 0 || W <= 0) return DP_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(pts_count_kernel, dim3(H), dim3(256), 0, s, depth, W, row_offsets);
+  hipLaunchKernelGGL(pts_scan_kernel, dim3(1), dim3(1024), 0, s, row_offsets, H);
+  hipLaunchKernelGGL(pts_scatter_kernel, dim3(H), dim3(256), 0, s, depth, H, W, f_px_dev, f_px, use_given, rgb_hwc,
+                     row_offsets, xyz, rgb_out);
+  DP_CHECK_LAUNCH();
+  return 0;
+}

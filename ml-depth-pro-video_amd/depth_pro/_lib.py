@@ -33,6 +33,7 @@ EXPORTS = (
     "dp_abi_version", "dp_gemm", "dp_layernorm", "dp_attention", "dp_normalize_u8",
     "dp_resize_bilinear", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
     "dp_fov_tail", "dp_infer_epilogue", "dp_gemm_workspace_size", "dp_gemm_plan",
+    "dp_depth_to_points",
 )
 
 
@@ -101,6 +102,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "dp_fov_tail": [vp, i32, vp, f32, vp, vp],
         "dp_infer_epilogue": [vp, i32, i32, vp, i32, f64, i32, i32, vp, vp, vp],
         "dp_gemm_workspace_size": [],
+        "dp_depth_to_points": [vp, i32, i32, vp, f64, i32, vp, vp, vp, vp, vp],
         "dp_gemm_plan": [ctypes.POINTER(GemmArgs), ctypes.POINTER(i32), ctypes.POINTER(i32)],
     }
     for name, argtypes in sig.items():

@@ -34,6 +34,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import depth_pro  # noqa: E402  (this package's drop-in)
 from depth_pro import distributed as D  # noqa: E402
+from depth_pro import pointcloud as PC  # noqa: E402
 
 
 def colorize_depth(depth, min_depth=None, max_depth=None, cmap="turbo"):
@@ -143,9 +144,25 @@ def generate_depth_map(image_path, output_path=None, downscale_factor=1.0, half_
         return None
 
 
+def _points(depth: torch.Tensor, f_px, image: np.ndarray, device: torch.device):
+    """Camera-space point cloud of one frame on the GPU (depth_to_3d, img_to_normalized_pointcloud.py:819-856)."""
+    h, w = depth.shape
+    rgb = torch.from_numpy(np.ascontiguousarray(image)).to(device, non_blocking=True)
+    pts, _, cols = PC.depth_to_3d(depth, f_px, w, h, rgb=rgb)
+    host_p = torch.empty(pts.shape, dtype=pts.dtype, pin_memory=True)
+    host_c = torch.empty(cols.shape, dtype=cols.dtype, pin_memory=True)
+    host_p.copy_(pts, non_blocking=True)
+    host_c.copy_(cols, non_blocking=True)
+    return host_p, host_c
+
+
 def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_factor=1.0, half_precision=False,
-                              colored=True, cmap="turbo", decode_workers=4, encode_workers=4):
-    """Directory loop (reference :153-206), pipelined decode -> GPU -> encode, frame-sharded across ranks."""
+                              colored=True, cmap="turbo", decode_workers=4, encode_workers=4, pointcloud=False):
+    """Directory loop (reference :153-206), pipelined decode -> GPU -> encode, frame-sharded across ranks.
+
+    pointcloud=True also writes `{base}_points.ply` per frame: the reference's depth_to_3d
+    back-projection with the frame's focal length (EXIF, or the FOV head's) and RGB colours
+    (the reference's ground-plane normalisation is out of scope)."""
     os.makedirs(output_dir, exist_ok=True)
     image_paths = sorted(glob.glob(os.path.join(input_dir, pattern)))
     if not image_paths:
@@ -173,14 +190,18 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                     futs[mine[nxt]] = dec.submit(_load, image_paths[mine[nxt]], downscale_factor)
                     nxt += 1
                 with torch.no_grad():
-                    depth = model.infer(transform(image), f_px=f_px)["depth"]
+                    pred = model.infer(transform(image), f_px=f_px)
+                    depth = pred["depth"]
                 host = torch.empty(depth.shape, dtype=depth.dtype, pin_memory=True)
                 host.copy_(depth, non_blocking=True)
+                pc = _points(depth, pred["focallength_px"], image, device) if pointcloud else None
                 ev = torch.cuda.Event()
                 ev.record()
 
-                def _finish(host=host, ev=ev, path=output_path):
+                def _finish(host=host, ev=ev, path=output_path, pc=pc, base=base_name):
                     ev.synchronize()
+                    if pc is not None:
+                        PC.write_ply(os.path.join(output_dir, f"{base}_points.ply"), pc[0].numpy(), pc[1].numpy())
                     return _encode(host.numpy(), path, colored, cmap)
 
                 pending.append(enc.submit(_finish))
@@ -206,13 +227,15 @@ def main():
                         help="Downscale input images for faster processing")
     parser.add_argument("--half_precision", action="store_true", help="Use float16 for faster computation")
     parser.add_argument("--raw", action="store_true", help="Save raw depth maps (grayscale) instead of colored ones")
+    parser.add_argument("--pointcloud", action="store_true",
+                        help="Also write {frame}_points.ply (depth_to_3d back-projection with RGB colours)")
     parser.add_argument("--colormap", type=str, default="turbo",
                         choices=["turbo", "viridis", "plasma", "inferno", "magma", "cividis", "jet"],
                         help="Colormap for depth visualization")
     args = parser.parse_args()
     batch_generate_depth_maps(input_dir=args.input_dir, output_dir=args.output_dir, pattern=args.pattern,
                               downscale_factor=args.downscale_factor, half_precision=args.half_precision,
-                              colored=not args.raw, cmap=args.colormap)
+                              colored=not args.raw, cmap=args.colormap, pointcloud=args.pointcloud)
 
 
 if __name__ == "__main__":

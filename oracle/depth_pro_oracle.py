@@ -246,3 +246,21 @@ def transform(img_u8) -> torch.Tensor:
     """depth_pro.py:125-132 Compose: ToTensor, Normalize(.5,.5), fp32."""
     t = torch.from_numpy(img_u8).permute(2, 0, 1).contiguous().to(torch.float32).div(255.0)
     return (t - 0.5) / 0.5
+
+
+# --------------------------------------------------------------- point cloud
+def depth_to_3d(depth_in, focallength_px, width, height):
+    """Reference `depth_to_3d` (img_to_normalized_pointcloud.py:819-856), restated in numpy
+    (that module imports open3d / cv2 at the top, so it cannot be imported here).
+    Returns (points_3d (N, 3) float64, valid_mask (height, width) bool)."""
+    import numpy as np
+
+    depth_np = np.asarray(depth_in)
+    y_indices, x_indices = np.indices((height, width))
+    cx = width / 2
+    cy = height / 2
+    valid_mask = ~np.isnan(depth_np) & (depth_np > 0)
+    z = depth_np[valid_mask].flatten()
+    x = -1 * (x_indices[valid_mask] - cx) * z / focallength_px
+    y = -1 * (y_indices[valid_mask] - cy) * z / focallength_px
+    return np.column_stack((x, y, z)), valid_mask

@@ -56,3 +56,29 @@ def test_batch_loop_on_gpu(tmp_path, cuda):
     assert n_raw == 3
     raw = np.asarray(Image.open(tmp_path / "raw" / "output_0001_depth.png"))
     assert raw.shape == (360, 640)
+
+
+@pytest.mark.gpu
+def test_batch_loop_pointcloud_on_gpu(tmp_path, cuda):
+    """--pointcloud: one PLY per frame == depth_to_3d(infer depth, infer f_px) with the frame's colours."""
+    from PIL import Image
+
+    import torch
+
+    from depth_pro import pointcloud as PC
+    from oracle import depth_pro_oracle as O
+
+    src = tmp_path / "frames"
+    src.mkdir()
+    img = np.random.default_rng(5).integers(0, 256, (270, 480, 3), dtype=np.uint8)
+    Image.fromarray(img).save(src / "output_0000.png")
+    out = tmp_path / "pc"
+    assert G.batch_generate_depth_maps(str(src), str(out), pattern="output_*.png", pointcloud=True) == 1
+    pts, cols = PC.read_ply(str(out / "output_0000_points.ply"))
+    model, transform = G._model(cuda, False)
+    with torch.no_grad():
+        pred = model.infer(transform(img))
+    depth = pred["depth"].cpu().numpy()
+    ref, valid = O.depth_to_3d(depth, float(pred["focallength_px"]), 480, 270)
+    assert np.array_equal(pts, ref)
+    assert np.array_equal(cols, img[valid])
