@@ -63,9 +63,9 @@ def _write_png(path: str, arr: np.ndarray) -> None:
     from PIL import Image
 
     if arr.dtype == np.uint16:
-        Image.fromarray(arr, mode="I;16").save(path)
+        Image.fromarray(np.ascontiguousarray(arr)).save(path)          # 16-bit greyscale (I;16)
     else:
-        Image.fromarray(arr, mode="RGB").save(path, compress_level=1)
+        Image.fromarray(np.ascontiguousarray(arr)).save(path, compress_level=1)
 
 
 def _resize_u8(image: np.ndarray, factor: float) -> np.ndarray:
