@@ -504,8 +504,10 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
 
 template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU>
 __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
-  constexpr int WN = 4;
-  constexpr int TM = BM / 2, TN = BN / WN;
+  // 8 waves as WM x WN; the 512 x 128 tile (N = 128 layers) uses 4 x 2 so that every
+  // wave still owns a 128 x 64 sub-tile (same fragment reuse as the 256 x 256 tile)
+  constexpr int WN = BM == 512 ? 2 : 4, WM = 8 / WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int RB = BKT * 2;                 // LDS row bytes
   constexpr int CR = BKT / 8;                 // 16-B chunks per row
@@ -524,7 +526,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WN, wn = wave % WN;
 
   // XCD-aware bijective remap (blocks b and b+8 share an XCD under round-robin dispatch)
   const int nwg = gridDim.x, bid = blockIdx.x;
@@ -766,7 +768,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
       ms[it] = m0 + wm * TM + q * 32 + row;
     }
-    if constexpr (TN == 32) {
+    if constexpr (TN % 32 == 0) {
       if (p.store_mode == DP_STORE_HEAD_PS) {
         head_ps_rows<NIT>(p, cc, ms, n_l, v, lane);
         continue;
@@ -1446,6 +1448,7 @@ int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
     case DP_TILE_DEEP5_256x256: return launch_big<K_, 256, 256, 32, 5, false>(p, conv, s);
     case DP_TILE_DEEP_256x128: return launch_big<K_, 256, 128, 32, 6, false>(p, conv, s);
     case DP_TILE_BIG_320x256: return launch_big<K_, 320, 256, 64, 2, false>(p, conv, s);
+    case DP_TILE_BIG_512x128: return launch_big<K_, 512, 128, 64, 2, false>(p, conv, s);
     default: return launch_big<K_, 256, 256, 64, 2, false>(p, conv, s);
   }
 }
@@ -1497,7 +1500,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
   tile = a->tile;
   if (a->store_mode == DP_STORE_HEAD_PS) {
-    tile = DP_TILE_BIG_256x128;   // TN = 32: one parity group per wave column
+    // 32-column parity groups must not straddle a wave's columns (TN = 32 or 64)
+    tile = a->M >= 512 * 256 ? DP_TILE_BIG_512x128 : DP_TILE_BIG_256x128;
   } else if (a->head_w) {
     if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;
     tile = DP_TILE_256x32;
@@ -1508,8 +1512,14 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     if (a->N <= 32) tile = DP_TILE_256x32;
     else if (a->N <= 64) tile = DP_TILE_256x64;
     else if (a->N % 8 != 0) tile = DP_TILE_128x128;
+    else if (a->N == 128 && a->M >= 512 * 256) tile = DP_TILE_BIG_512x128;   // N = 128 convs at 768^2
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
-    else {
+    else if (ws_ok && a->K <= 256 && tiles256 >= 1024) {
+      // short-K, many tiles (the 384^2 -> 768^2 deconvs: 4 K steps per tile): the
+      // persistent stream-K engine keeps the next tile's loads in flight under each
+      // epilogue, which otherwise dominates (tools/gemm_bench.py: 162 vs 198 us)
+      tile = DP_TILE_STREAMK_256x256;
+    } else {
       // Wide-N GEMMs: 256 x 256 tiles (8-phase engine once there are >= 600 of
       // them: tools/gemm_bench.py), or 320 x 256 when that needs fewer rounds of
       // workgroups over the CUs per unit of tile work -- e.g. the ViT's M = 20195
@@ -1565,6 +1575,7 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
     case DP_TILE_128x128: bm = 128; bn = 128; break;
     case DP_TILE_BIG_256x128: case DP_TILE_BIG_256x128_K32: case DP_TILE_DEEP_256x128: bn = 128; break;
     case DP_TILE_BIG_320x256: bm = 320; bn = 256; break;
+    case DP_TILE_BIG_512x128: bm = 512; bn = 128; break;
     default: bn = 256;
   }
   if (tile_out) *tile_out = tile;

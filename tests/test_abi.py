@@ -80,6 +80,7 @@ def test_gemm_plan_tile_choice():
     assert plan(20195, 1024, 1024)[1:] == (_lib.DP_TILE_BIG_320x256, 64 * 4)     # one round on 256 CUs
     assert plan(20195, 4096, 1024)[1:] == (_lib.DP_TILE_8PH_256x256, 79 * 16)
     assert plan(577, 3072, 1024)[1:] == (_lib.DP_TILE_BIG_256x128, 3 * 24)       # side encoders
+    assert plan(768 * 768, 128, 2304)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)     # head.0 conv (N = 128)
     # stream-K is opt-in and needs a workspace
     assert plan(20195, 3072, 1024, tile=_lib.DP_TILE_STREAMK_256x256)[0] == 1000
     ws = lib.dp_gemm_workspace_size()

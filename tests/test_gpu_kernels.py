@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 
 from depth_pro import ops  # noqa: E402
 from depth_pro._lib import (DP_ACT_GELU, DP_ACT_RELU, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa: E402
-                            DP_TILE_BIG_256x256, DP_TILE_BIG_320x256, DP_TILE_STREAMK_256x256)
+                            DP_TILE_BIG_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_512x128,
+                            DP_TILE_STREAMK_256x256)
 
 DTYPES = [torch.bfloat16, torch.float16]
 
@@ -321,7 +322,8 @@ def test_gemm_stream_k_conv3x3_relu_residual(cuda, dt):
     close(out.reshape(1, S, S, C).permute(0, 3, 1, 2), ref, dt, "stream-K conv3x3")
 
 
-ENGINES = [DP_TILE_BIG_256x256, DP_TILE_8PH_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_256x128, DP_TILE_STREAMK_256x256]
+ENGINES = [DP_TILE_BIG_256x256, DP_TILE_8PH_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_256x128, DP_TILE_BIG_512x128,
+           DP_TILE_STREAMK_256x256]
 
 
 @pytest.mark.parametrize("tile", ENGINES)

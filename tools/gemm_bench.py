@@ -10,12 +10,13 @@ from depth_pro import ops  # noqa: E402
 from depth_pro._lib import (DP_TILE_128x128, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa
                             DP_TILE_BIG_256x128_K32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32,
                             DP_TILE_DEEP4_256x256, DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128,
-                            DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256)
+                            DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_512x128)
 
 TILES = (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
          ("8ph256x256", DP_TILE_8PH_256x256), ("deep4_256x256", DP_TILE_DEEP4_256x256),
          ("deep5_256x256", DP_TILE_DEEP5_256x256), ("deep6_256x128", DP_TILE_DEEP_256x128),
-         ("sk256x256", DP_TILE_STREAMK_256x256), ("big320x256", DP_TILE_BIG_320x256))
+         ("sk256x256", DP_TILE_STREAMK_256x256), ("big320x256", DP_TILE_BIG_320x256),
+         ("small128x128", DP_TILE_128x128), ("big512x128", DP_TILE_BIG_512x128))
 N256 = (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
         DP_TILE_DEEP5_256x256, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256)
 
@@ -27,6 +28,9 @@ SHAPES = [  # (name, M, N, K, kw)
     ("conv3x3 768^2 256->256", 768 * 768, 256, 2304, {"conv": 768}),
     ("conv3x3 384^2 256->256", 384 * 384, 256, 2304, {"conv": 384}),
     ("head conv 768^2 256->128", 768 * 768, 128, 2304, {"conv": 768}),
+    ("composed head 768^2 128->4x32", 768 * 768, 128, 1152, {"conv": 768}),
+    ("deconv 384->768 256ch", 384 * 384, 1024, 256, {"deconv": (384, 384, 256)}),
+    ("deconv 192->384 256ch", 192 * 192, 1024, 256, {"deconv": (192, 192, 256)}),
 ]
 
 
@@ -71,6 +75,7 @@ def main():
             A = torch.randn(M, K, device=dev, generator=g).to(dt)
             conv = None
         C = torch.zeros(M, N, device=dev, dtype=torch.float32 if kw.get("acc") else dt)
+        dc = kw.get("deconv")
         flop = 2.0 * M * N * K
         res = []
         for tname, tile in (() if args.torch_only else TILES):
@@ -79,7 +84,8 @@ def main():
             if args.tile and tname not in args.tile.split(","):
                 continue
             f = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, conv=conv, bias=bias, act=2 if kw.get("gelu") else 0,
-                                 accumulate=bool(kw.get("acc")), tile=tile, workspace=ws)  # noqa: E731
+                                 accumulate=bool(kw.get("acc")), tile=tile, workspace=ws, deconv=dc,
+                                 ldc=dc[2] if dc else None)  # noqa: E731
             ms = timeit(f, args.iters)
             res.append(f"{tname} {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
             if args.ablate and tname.startswith("big"):
@@ -91,7 +97,7 @@ def main():
                 _lib.load().dp_gemm_debug_flags(0)
                 res.append("[" + " ".join(parts) + "]")
         # correctness of the big engine vs the small one on this shape
-        if not kw.get("acc") and not args.tile and not args.torch_only:
+        if not kw.get("acc") and not dc and not args.tile and not args.torch_only:
             C1 = torch.empty_like(C)
             ops.gemm(A, B, C1, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_128x128)
             C2 = torch.empty_like(C)
@@ -102,7 +108,7 @@ def main():
                 ops.gemm(A, B, C2, M=M, N=N, K=K, conv=conv, bias=bias, tile=t, workspace=ws)
                 d = max(d, (C1.float() - C2.float()).abs().max().item())
             res.append(f"max|small-big|={d:.2e}")
-        if conv is None and (not args.tile or args.torch_only):
+        if conv is None and not dc and (not args.tile or args.torch_only):
             ms = timeit(lambda: torch.matmul(A, B.t()))
             res.append(f"torch.matmul {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
         print(f"{name:28s} " + " | ".join(res), flush=True)
