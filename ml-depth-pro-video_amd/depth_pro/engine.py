@@ -243,6 +243,9 @@ class Engine:
         self.ws_main = ops.gemm_workspace(dev)
         self.ws_side = ops.gemm_workspace(dev)
         self.serial_side = False   # True: run the side encoders on the current stream (profiling)
+        # FOV encoder + head beside the decoder instead of the patch encoder (measured: 0.3 ms
+        # slower on MI355X, so off by default; DP_FOV_LATE=1 to try)
+        self.fov_late = os.environ.get("DP_FOV_LATE", "0") == "1"
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
@@ -311,19 +314,30 @@ class Engine:
         return self.feats
 
     # -------------------------------------------------------------- forward
-    def _side_encoders(self):
-        """Image encoder (+ lowres upsample) and FOV encoder (+ Linear): ~5 % of the
-        frame's FLOPs at M = 577 rows, far too few tiles to fill 256 CUs alone, so
-        they run on a side stream and fill the patch encoder's idle CUs."""
+    def _image_encoder(self):
+        """Image encoder (+ lowres upsample): ~2.5 % of the frame's FLOPs at M = 577
+        rows, far too few tiles to fill 256 CUs alone, so it runs on a side stream
+        beside the patch encoder."""
         P, e = self.P, "encoder."
         self._vit("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
         ops.merge_windows(self.vi.h, 0, 1, 0, self.g)
         self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
                      C_off=D, ldc=2 * D)
-        if self.use_fov:
-            vf = self.vf
-            self._vit("fov.encoder.0.", vf, 1, 34 * PTOK)
-            ops.gemm(vf.h, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
+
+    def _fov_encoder(self):
+        """FOV encoder ViT + Linear (fov.py:45-47, 66-72)."""
+        vf, P = self.vf, self.P
+        self._vit("fov.encoder.0.", vf, 1, 34 * PTOK)
+        ops.gemm(vf.h, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
+
+    def _fov_head(self):
+        """FOV head (fov.py:56-82): needs the low-res decoder features and the FOV tokens."""
+        P = self.P
+        self._conv3(self.low, 48, 256, P["fov.down.w"], self.fx, 128, bias=P["fov.down.b"], act=DP_ACT_RELU,
+                    R1=self.fov_tok, stride=2)
+        self._conv3(self.fx, 24, 128, P["fov.h0.w"], self.f12, 64, bias=P["fov.h0.b"], act=DP_ACT_RELU, stride=2)
+        self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
+        ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
 
     def forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
         """Run the network on `self.x0`; results in self.canonical / self.fov_deg."""
@@ -334,19 +348,27 @@ class Engine:
         """Body of `forward`.
 
         Two streams: the current stream runs the patch encoder -> decoder -> head;
-        `self.side` runs the image + FOV encoders (forked after the window
-        im2col, joined before fuse_lowres / the FOV head).
+        `self.side` runs the image encoder beside the patch encoder (forked after
+        the window im2col, joined before fuse_lowres), then -- `fov_late` -- the
+        FOV encoder + FOV head beside the decoder (forked once the low-res
+        decoder features exist, joined at the end), so that only one M = 577
+        encoder competes with the patch encoder's full-chip GEMMs.
         """
         P = self.P
         main = torch.cuda.current_stream(self.dev)
+        side_ok = "side" not in _ABLATE
         ops.patchify_pyramid(self.x0, self.cols)
         if self.serial_side:
-            self._side_encoders()
+            self._image_encoder()
+            if self.use_fov:
+                self._fov_encoder()
         else:
             self.side.wait_stream(main)
             with torch.cuda.stream(self.side), ops.use_workspace(self.ws_side):
-                if "side" not in _ABLATE:
-                    self._side_encoders()
+                if side_ok:
+                    self._image_encoder()
+                    if self.use_fov and not self.fov_late:
+                        self._fov_encoder()
         vp = self.vp
         hooks = {
             5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
@@ -376,12 +398,15 @@ class Engine:
         ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
         self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)
-        if self.use_fov:  # FOV head (fov.py:56-82) only needs the lowres features
-            self._conv3(self.low, 48, 256, P["fov.down.w"], self.fx, 128, bias=P["fov.down.b"], act=DP_ACT_RELU,
-                        R1=self.fov_tok, stride=2)
-            self._conv3(self.fx, 24, 128, P["fov.h0.w"], self.f12, 64, bias=P["fov.h0.b"], act=DP_ACT_RELU, stride=2)
-            self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
-            ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
+        fov_side = self.use_fov and self.fov_late and not self.serial_side
+        if self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
+            self._fov_head()
+        elif fov_side:
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side), ops.use_workspace(self.ws_side):
+                if side_ok:
+                    self._fov_encoder()
+                    self._fov_head()
         if "decoder" not in _ABLATE:
             f = self._fusion(4, self.low, 48, None)
             for i, (enc, s, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)), (1, (self.enc1, 384, 256))):
@@ -391,6 +416,8 @@ class Engine:
             feats = self._fusion(0, f, 768, self.enc0)
         else:
             feats = self.feats
+        if fov_side:
+            main.wait_stream(self.side)
         if "head" in _ABLATE:
             return self.canonical, self.fov_deg
         # head (depth_pro.py:182-207): conv3x3, then deconv -> conv3x3 -> ReLU -> 1x1 -> ReLU as ONE
