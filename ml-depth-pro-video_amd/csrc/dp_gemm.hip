@@ -757,24 +757,30 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       #pragma unroll
       for (int j = 0; j < FN; ++j)
         *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[2 * q + i][j];
-    float v[NIT][8];
-    int ms[NIT];
+    // rows of per-row operands batched per epilogue call: all of a pass's rows, except
+    // for the 128-160-row wave tiles whose accumulators leave room for only 2 at a time
+    constexpr int NITC = FM >= 8 && NIT > 2 ? 2 : NIT;
     #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int row = it * RPI + lane / CPR;
-      const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
-      const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+    for (int c0 = 0; c0 < NIT; c0 += NITC) {
+      float v[NITC][8];
+      int ms[NITC];
       #pragma unroll
-      for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
-      ms[it] = m0 + wm * TM + q * 32 + row;
-    }
-    if constexpr (TN % 32 == 0) {
-      if (p.store_mode == DP_STORE_HEAD_PS) {
-        head_ps_rows<NIT>(p, cc, ms, n_l, v, lane);
-        continue;
+      for (int it = 0; it < NITC; ++it) {
+        const int row = (c0 + it) * RPI + lane / CPR;
+        const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
+        const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
+        ms[it] = m0 + wm * TM + q * 32 + row;
       }
+      if constexpr (TN % 32 == 0) {
+        if (p.store_mode == DP_STORE_HEAD_PS) {
+          head_ps_rows<NITC>(p, cc, ms, n_l, v, lane);
+          continue;
+        }
+      }
+      epilogue_rows<K_, NITC>(p, cc, ms, n_l, v);
     }
-    epilogue_rows<K_, NIT>(p, cc, ms, n_l, v);
   }
   DP_STAMP(st3_);
   DP_STAMP_SAVE(wgid);
@@ -946,18 +952,21 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
       #pragma unroll
       for (int j = 0; j < 4; ++j)
         *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[2 * q + i][j];
-    float v[NIT][8];
-    int ms[NIT];
     #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int row = it * RPI + lane / CPR;
-      const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
-      const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+    for (int c0 = 0; c0 < NIT; c0 += 2) {     // 2 rows per call: 128 accumulators still live
+      float v[2][8];
+      int ms[2];
       #pragma unroll
-      for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
-      ms[it] = m0 + wm * TM + q * 32 + row;
+      for (int it = 0; it < 2; ++it) {
+        const int row = (c0 + it) * RPI + lane / CPR;
+        const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
+        const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
+        ms[it] = m0 + wm * TM + q * 32 + row;
+      }
+      epilogue_rows<K_, 2>(p, cc, ms, n_l, v);
     }
-    epilogue_rows<K_, NIT>(p, cc, ms, n_l, v);
   }
 }
 
