@@ -32,9 +32,10 @@ PEAK_HBM_GBS = 8000.0
 
 
 TILE_NAMES = {1: "128x128", 2: "256x64", 3: "256x32", 4: "256x256", 5: "256x128", 8: "8phase-256x256",
-              12: "streamK-256x256", 13: "320x256"}
+              12: "streamK-256x256", 13: "320x256", 14: "512x128"}
 TILE_KERNEL = {1: "gemm_kernel<KBF16, 128, 128", 4: "gemm_big_kernel<KBF16, 256, 256", 5: "gemm_big_kernel<KBF16, 256, 128",
-               8: "gemm_8ph_kernel<KBF16", 12: "gemm_sk_kernel<KBF16", 13: "gemm_big_kernel<KBF16, 320, 256"}
+               8: "gemm_8ph_kernel<KBF16", 12: "gemm_sk_kernel<KBF16", 13: "gemm_big_kernel<KBF16, 320, 256",
+               14: "gemm_big_kernel<KBF16, 512, 128"}
 
 
 def pmc_traffic(kernel: str, workgroups: int):
