@@ -55,12 +55,16 @@ def main():
     ap.add_argument("--tile", default=None, help="128x128 | big256x256 | big256x128")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch-only", action="store_true", help="time only torch.matmul (hipBLASLt) on the dense shapes")
+    ap.add_argument("--dbg", type=int, default=0, help="dp_gemm_debug_flags for every run (8 = direct epilogue)")
     ap.add_argument("--ablate", action="store_true", help="time the no-store / no-load / no-mfma variants")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     dt = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(0)
     ws = ops.gemm_workspace(dev)
+    if args.dbg:
+        from depth_pro import _lib
+        _lib.load().dp_gemm_debug_flags(args.dbg)
     for name, M, N, K, kw in SHAPES:
         if args.only and args.only not in name:
             continue
@@ -94,7 +98,7 @@ def main():
                 for flags, lab in ((1, "nostore"), (2, "noload"), (3, "nostore+noload"), (4, "nomfma"), (5, "nomfma+nostore")):
                     _lib.load().dp_gemm_debug_flags(flags)
                     parts.append(f"{lab} {timeit(f, args.iters)*1e3:.1f}")
-                _lib.load().dp_gemm_debug_flags(0)
+                _lib.load().dp_gemm_debug_flags(args.dbg)
                 res.append("[" + " ".join(parts) + "]")
         # correctness of the big engine vs the small one on this shape
         if not kw.get("acc") and not dc and not args.tile and not args.torch_only:
