@@ -417,6 +417,27 @@ __device__ __forceinline__ void head_ps_rows(const GemmP& p, const ColConst& cc,
   }
 }
 
+
+// Tile order within the XCD-contiguous workgroup ranges.  Row-major (tile_n fastest)
+// puts the 32 workgroups an XCD runs at once on ~2 rows of tiles x all columns;
+// with BAND > 1 they sweep bands of BAND tile rows column by column instead, so the
+// tiles in flight on one XCD form a squarer block (e.g. 4 x 8) that shares fewer
+// distinct A / B panels in its 4 MiB L2: qkv 155 -> 150 us, fc1 197 -> 190 us
+// (tools/gemm_bench.py --dbg 16 restores row-major, for A/B).
+__device__ __forceinline__ void tile_coords(const GemmP& p, int wgid, int& tile_m, int& tile_n) {
+  const int band = (p.dbg & 16) ? 1 : 4;
+  const int tm_full = p.tiles_m / band * band;       // rows covered by whole bands
+  const int per_band = band * p.tiles_n;
+  if (band > 1 && wgid < tm_full * p.tiles_n) {
+    const int b = wgid / per_band, r = wgid - b * per_band;
+    tile_n = r / band;
+    tile_m = b * band + (r - tile_n * band);
+  } else {
+    tile_n = wgid % p.tiles_n;
+    tile_m = wgid / p.tiles_n;
+  }
+}
+
 // implicit-conv row descriptor: output pixel m -> top-left input tap
 struct ConvRow {
   int iy, ix, pix;
@@ -532,7 +553,8 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
+  int tile_m, tile_n;
+  tile_coords(p, wgid, tile_m, tile_n);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   DP_STAMPS_DECL;
   DP_STAMP(st0_);
@@ -814,7 +836,8 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile_n = wgid % p.tiles_n, tile_m = wgid / p.tiles_n;
+  int tile_m, tile_n;
+  tile_coords(p, wgid, tile_m, tile_n);
   const int m0 = tile_m * 256, n0 = tile_n * 256;
 
   // LDS-DMA pieces: half-tile row r = i*64 + wave*8 + lane/8 (i = 0,1), swizzle on the source
@@ -974,7 +997,8 @@ template <typename K_>
 int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
   GemmP p = p0;
   p.tiles_n = (p.N + 255) / 256;
-  dim3 grid(p.tiles_n * ((p.M + 255) / 256));
+  p.tiles_m = (p.M + 255) / 256;
+  dim3 grid(p.tiles_n * p.tiles_m);
   if (conv && p.relu_a) hipLaunchKernelGGL((gemm_8ph_kernel<K_, true, true>), grid, dim3(512), 0, s, p);
   else if (conv) hipLaunchKernelGGL((gemm_8ph_kernel<K_, true, false>), grid, dim3(512), 0, s, p);
   else if (p.relu_a) hipLaunchKernelGGL((gemm_8ph_kernel<K_, false, true>), grid, dim3(512), 0, s, p);

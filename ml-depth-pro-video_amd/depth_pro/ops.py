@@ -179,9 +179,37 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
         t, g = ctypes.c_int32(), ctypes.c_int32()
         check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
         return t.value, g.value
+    _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None)
     kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
     with _Timed(kind, 2.0 * M * N * K, (M, N, K)):
         check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
+
+
+def _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head, head_ps) -> None:
+    """Host-side bounds check: every element dp_gemm will read or write lies inside the
+    tensors passed (a wrong leading dimension would otherwise write past the buffer on
+    the GPU)."""
+    def need(t, off, n, what):
+        if off + n > t.numel():
+            raise _lib.DPError(f"dp_gemm: {what} needs {off + n} elements, tensor has {t.numel()}")
+
+    M, N, K = a.M, a.N, a.K
+    if conv is not None:
+        need(A, A_off, (M // (a.out_h * a.out_w)) * a.in_h * a.in_w * a.in_c, "A (conv input)")
+    else:
+        need(A, A_off, (M - 1) * a.lda + K, "A")
+    need(B, 0, (N - 1) * a.ldb + K, "B")
+    if head_ps:
+        need(C, C_off, (M // (a.out_h * a.out_w)) * 4 * a.out_h * a.out_w, "C (pixel-shuffle head)")
+    elif head:
+        need(C, C_off, M, "C (fused head)")
+    elif deconv is not None:
+        need(C, C_off, (4 * M - 1) * a.ldc + a.dc_cout, "C (deconv)")
+    else:
+        last = M - 1
+        if a.row_group:
+            last = (last // a.row_group) * a.row_group_out + a.row_off + last % a.row_group
+        need(C, C_off, last * a.ldc + N, "C")
 
 
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor, rows: int, cols: int,
