@@ -60,6 +60,33 @@ def frame(seed: int) -> np.ndarray:
     return np.random.default_rng(seed=seed).integers(0, 256, (1536, 1536, 3), dtype=np.uint8)
 
 
+def depth_parity(depth: torch.Tensor, canonical: torch.Tensor, fov: torch.Tensor) -> dict:
+    """The "+ depth L1 vs reference" half of the metric, on synthetic frame 0 / seed-0 weights.
+
+    Reference = tests/golden/golden_forward_frame0.npz (the reference's own DepthPro.forward on
+    the same frame and weights, tests/golden/make_golden.py): canonical inverse depth every 8th
+    pixel + fov_deg.  Its depth follows the reference infer epilogue (depth_pro.py:282-298):
+    f_px = 0.5 W / tan(0.5 rad(fov)); depth = 1 / clamp(canonical * W / f_px, 1e-4, 1e4).
+    Metric: relative L1 = mean|x - x_ref| / mean|x_ref| over the 192 x 192 grid.
+    """
+    path = os.path.join(REPO, "tests", "golden", "golden_forward_frame0.npz")
+    if not os.path.exists(path):
+        return None
+    g = np.load(path)
+    c_ref = g["canonical_sub8"].astype(np.float64)
+    fov_ref = float(g["fov_deg"][0])
+    W = 1536.0
+    f_ref = 0.5 * W / np.tan(0.5 * np.deg2rad(fov_ref))
+    d_ref = 1.0 / np.clip(c_ref * (W / f_ref), 1e-4, 1e4)
+    d = depth[::8, ::8].double().cpu().numpy()
+    c = canonical.reshape(1536, 1536)[::8, ::8].double().cpu().numpy()
+    rel = lambda a, b: float(np.abs(a - b).mean() / np.abs(b).mean())  # noqa: E731
+    return {"depth_rel_l1": round(rel(d, d_ref), 7), "canonical_rel_l1": round(rel(c, c_ref), 7),
+            "fov_rel_err": round(abs(float(fov.reshape(-1)[0]) - fov_ref) / fov_ref, 7),
+            "target": 1e-3, "frame": "synthetic frame 0 (1536x1536), graph replay, every 8th pixel",
+            "reference": "tests/golden/golden_forward_frame0.npz"}
+
+
 def cpu_baseline(seconds_cap: float = 60.0) -> dict:
     """The fp32 CPU oracle (a port of the reference path) on one synthetic frame."""
     from depth_pro.weights import synthetic_state_dict
@@ -121,21 +148,33 @@ def main():
 
     # resident inputs: this rank's first `pool` frames of the stream (frame k -> rank k mod N), u8 in HBM
     frames = [torch.from_numpy(frame(k)).to(dev) for k in D.shard_frames(args.pool * world, rank, world)]
-    depth = torch.empty(1536, 1536, dtype=torch.float32, device=dev)
+    # two depth buffers: frame i's gather to rank 0 (RCCL, its own stream) runs while
+    # frame i+1 computes; the buffer is reused only after its gather's work.wait()
+    depths = [torch.empty(1536, 1536, dtype=torch.float32, device=dev) for _ in range(2)]
+    depth = depths[0]
     fpx = torch.empty((), dtype=torch.float32, device=dev)
-    gathered = []
+    pending = [None, None]
 
     def step(i):
+        d = depths[i & 1]
+        if pending[i & 1] is not None:
+            pending[i & 1].wait()
+            pending[i & 1] = None
         ops.normalize_u8(frames[i % len(frames)], eng.x0)
         c, fov = eng.run()
-        ops.infer_epilogue(c, fov, None, 1536, 1536, depth, fpx)
+        ops.infer_epilogue(c, fov, None, 1536, 1536, d, fpx)
         if world > 1:
-            g = D.gather_frames(depth, dst=0)
-            if rank == 0 and len(gathered) < 2:
-                gathered.append(g)
+            _, pending[i & 1] = D.gather_frames(d, dst=0, async_op=True)
+
+    def drain():
+        for j in range(2):
+            if pending[j] is not None:
+                pending[j].wait()
+                pending[j] = None
 
     for i in range(args.warmup):
         step(i)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -143,6 +182,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -174,6 +214,14 @@ def main():
             k["launches"] += 1
             k["ms"] += ms
             k["flop"] += flops
+
+    parity = None
+    if rank == 0:
+        ops.normalize_u8(frames[0], eng.x0)          # rank 0 holds frame 0 of the stream
+        c, fov = eng.run()
+        ops.infer_epilogue(c, fov, None, 1536, 1536, depth, fpx)
+        torch.cuda.synchronize()
+        parity = depth_parity(depth, c, fov)
 
     if rank == 0:
         achieved = fps_per_gpu * FLOP_PER_FRAME / 1e12
@@ -230,6 +278,7 @@ def main():
                                    "basis": "fps_per_gpu x 19.247 TFLOP/frame (SURVEY 8d)"}},
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kern.items()},
+            "parity": parity,
             "setup_s": round(t_setup, 1),
         }
         if world == 1 and not args.no_cpu_baseline:

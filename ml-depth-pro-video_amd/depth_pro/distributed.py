@@ -66,14 +66,20 @@ def broadcast_packed(packed: Optional[Dict[str, object]], device: torch.device, 
     return out
 
 
-def gather_frames(t: torch.Tensor, dst: int = 0) -> Optional[List[torch.Tensor]]:
-    """Gather one equally-shaped tensor per rank to `dst` (rank order)."""
+def gather_frames(t: torch.Tensor, dst: int = 0, async_op: bool = False):
+    """Gather one equally-shaped tensor per rank to `dst` (rank order).
+
+    async_op=True returns (bufs, work): the gather runs on the collective's own
+    stream while the caller queues the next frame; `work.wait()` (which makes the
+    current stream, not the host, wait under RCCL) must precede any reuse of `t`
+    or read of `bufs`.
+    """
     world, rank = dist.get_world_size(), dist.get_rank()
     if world == 1:
-        return [t]
+        return ([t], None) if async_op else [t]
     bufs = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
-    dist.gather(t, gather_list=bufs, dst=dst)
-    return bufs
+    work = dist.gather(t, gather_list=bufs, dst=dst, async_op=async_op)
+    return (bufs, work) if async_op else bufs
 
 
 def order_results(per_step: Sequence[Sequence[torch.Tensor]], world: int) -> List[torch.Tensor]:

@@ -47,9 +47,25 @@ def _worker(rank, world, port, q):
             out = D.gather_frames(depth, dst=0)
             if rank == 0:
                 per_step.append(out)
+        # bench.py's pattern: two output buffers, asynchronous gathers, a buffer rewritten
+        # only after its previous gather's wait()
+        bufs = [torch.empty(4, 6), torch.empty(4, 6)]
+        pending, async_steps = [None, None], []
+        for i, k in enumerate(frames[:4]):
+            if pending[i & 1] is not None:
+                pending[i & 1][1].wait()
+                if rank == 0:
+                    async_steps.append([t.clone() for t in pending[i & 1][0]])
+            bufs[i & 1].fill_(float(k))
+            pending[i & 1] = D.gather_frames(bufs[i & 1], dst=0, async_op=True)
+        for j in (0, 1):
+            pending[j][1].wait()
+            if rank == 0:
+                async_steps.append([t.clone() for t in pending[j][0]])
         if rank == 0:
             order = [int(t[0, 0].item()) for t in D.order_results(per_step, world)]
             q.put(("order", order))
+            q.put(("async_order", [int(t[0, 0].item()) for t in D.order_results(async_steps, world)]))
         q.put(("rank", rank, frames, ok_bcast))
     finally:
         dist.destroy_process_group()
@@ -65,12 +81,13 @@ def test_frame_sharding_broadcast_gather_world2():
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    msgs = [q.get(timeout=5) for _ in range(world + 1)]
+    msgs = [q.get(timeout=5) for _ in range(world + 2)]
     ranks = {m[1]: m for m in msgs if m[0] == "rank"}
     assert ranks[0][2] == [0, 2, 4, 6, 8] and ranks[1][2] == [1, 3, 5, 7, 9]
     assert ranks[0][3] and ranks[1][3]
     order = [m[1] for m in msgs if m[0] == "order"][0]
     assert order == list(range(8))  # stream order restored at rank 0
+    assert [m[1] for m in msgs if m[0] == "async_order"][0] == list(range(8))
 
 
 def test_shard_frames_covers_stream_once():
