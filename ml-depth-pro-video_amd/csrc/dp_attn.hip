@@ -7,10 +7,13 @@
 // the online-softmax statistics are lane-local up to one permlane32 swap, and
 // the S^T accumulator registers, packed to 16 bits, are directly the B operand
 // of O^T = V^T . P^T (in a permuted key order that the V^T fragment matches).
-// K is staged row-major (padded rows, ds_read_b128); V is staged row-major too
-// and read transposed with ds_read_b64_tr_b16 (64-B halves XOR-swizzled on odd
-// row pairs: conflict-free).  Registers stage the next tile's K/V from HBM while
-// the current tile computes (one barrier per tile); Q stays in registers.
+// K and V tiles travel HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// wave-instruction, no staging registers): the next tile's DMA is in flight while
+// the current tile computes, one counted wait + barrier per tile.  Both are stored
+// as 128-B key rows with the 16-B chunk XOR-swizzled on the SOURCE address: K by
+// (row >> 1) & 7 (conflict-free ds_read_b128 of 16 rows), V by 64-B halves on odd
+// row pairs, read transposed with ds_read_b64_tr_b16 (conflict-free).  Q stays in
+// registers; 4 workgroups (16 waves) per CU.
 // Softmax: scale folded into one FMA per score, exp2, a deferred running-max
 // rescale, and row sums taken by the matrix core (an all-ones V^T block).
 // The last, partial key tile is masked and skips its empty 32-key half.
@@ -23,20 +26,37 @@ namespace {
 constexpr int QB = 128;      // queries per workgroup
 constexpr int KT = 64;       // keys per tile
 constexpr int HD = 64;       // head dim
-constexpr int KS = 72;       // K tile row stride (elements): conflict-free b128 reads
-constexpr int VRB = 128;     // V tile row bytes (64 d x 16 bit), swizzled
+constexpr int KS = 72;       // output staging row stride (elements): conflict-free b128 reads
+constexpr int VRB = 128;     // K / V tile row bytes (64 d x 16 bit), swizzled
+constexpr int TILE_B = KT * VRB;   // 8 KiB per operand tile
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int v_off(int row, int byte) {  // byte offset of (key row, byte in row)
   return row * VRB + (byte ^ (((row >> 1) & 1) << 6));
 }
+__device__ __forceinline__ int k_off(int row, int chunk) {  // byte offset of (key row, 16-B chunk)
+  return row * VRB + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// one 16-B-per-lane LDS-DMA piece at the wave-uniform LDS byte address `dst`
+// (inline asm: completion is tracked by the counted vmcnt wait in the tile loop)
+__device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
 
 template <typename K_>
-__global__ void __launch_bounds__(256, 3)
+__global__ void __launch_bounds__(256, 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
-  __shared__ __attribute__((aligned(16))) u16 sk[2][KT * KS];
-  __shared__ __attribute__((aligned(16))) char sv[2][KT * VRB];
+  __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // XCD-aware remap: workgroup i is dispatched to XCD i % 8, so consecutive work
@@ -66,32 +86,21 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     if (q < seq) qf[ks] = *(const uint4*)(base + (long long)q * ldq + qcol + 16 * ks + 8 * hi);
   }
 
-  // staging: thread -> (key row, 16-B d chunk) x 2.  Full tiles load without a
-  // predicate from row pointers that advance by one tile per step.
-  const int srow = tid >> 3, sch = tid & 7;
-  uint4 rk[2], rv[2];
-  const u16* kp = base + (long long)srow * ldq + kcol + 8 * sch;
-  const long long vk = vcol - kcol, row32 = 32 * ldq, tile_step = KT * ldq;
-  auto load = [&](int k0, bool full) {
-    const u16* r = kp + (long long)k0 * ldq;
+  // LDS-DMA staging: piece i of wave w fills key rows 32 i + 8 w + lane / 8, slot
+  // lane % 8 of each 128-B row; the slot holds logical chunk slot ^ swizzle(row), so
+  // the swizzle lives in the source address.  Rows past seq re-read row seq-1
+  // (finite, masked to -inf / weight 0 in the partial tile).
+  const int prow = wave * 8 + (lane >> 3), pslot = lane & 7;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(&smem[0][0]) + wave * 1024);
+  auto issue = [&](int k0, int buf) {
+    const uint32_t dk = __builtin_amdgcn_readfirstlane(lds0 + buf * 2 * TILE_B), dv = dk + TILE_B;
     #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      if (full || k0 + srow + 32 * i < seq) {
-        rk[i] = *(const uint4*)(r + i * row32);
-        rv[i] = *(const uint4*)(r + i * row32 + vk);
-      } else {
-        rk[i] = make_uint4(0, 0, 0, 0);
-        rv[i] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  (void)tile_step;
-  auto store = [&](int buf) {
-    #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = srow + 32 * i;
-      *(uint4*)(&sk[buf][key * KS + 8 * sch]) = rk[i];
-      *(uint4*)(&sv[buf][v_off(key, 16 * sch)]) = rv[i];
+      const int row = prow + 32 * i;
+      const int key = min(k0 + row, seq - 1);
+      const u16* r = base + (long long)key * ldq;
+      glds16(r + kcol + 8 * (pslot ^ ((row >> 1) & 7)), dk + i * 4096);
+      glds16(r + vcol + 8 * (pslot ^ (((row >> 1) & 1) << 2)), dv + i * 4096);
     }
   };
   // transposed V read address (bytes, within a stage) for the A operand of
@@ -118,8 +127,8 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     if (!active) return;
     const int cur = t & 1;
     const int kbase = t * KT;
-    const u16* K = sk[cur];
-    const char* V = sv[cur];
+    const char* K = smem[cur];
+    const char* V = smem[cur] + TILE_B;
     const bool two = !PARTIAL || kbase + 32 < seq;
     // ---- S^T for the two 32-key blocks
     f32x16_t s[2];
@@ -132,7 +141,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       }
       #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const uint4 kf = *(const uint4*)(K + (kb * 32 + l32) * KS + 16 * ks + 8 * hi);
+        const uint4 kf = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
         s[kb] = K_::mfma32(kf, qf[ks], ks == 0 ? f32x16_t{} : s[kb]);
       }
     }
@@ -202,24 +211,25 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     }
   };
 
+  // tile t lives in stage t & 1.  Top of step t: tile t's DMA was issued one step
+  // earlier (own pieces: vmcnt(0); everyone's: the barrier, which also certifies
+  // that every wave finished tile t-1, whose stage now receives tile t+1).
   const int ntiles = (seq + KT - 1) / KT, nfull = seq / KT;
-  load(0, nfull > 0);
-  store(0);
-  __syncthreads();
+  issue(0, 0);
   for (int t = 0; t < nfull; ++t) {
-    if (t + 1 < ntiles) load((t + 1) * KT, t + 1 < nfull);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + 1 < ntiles) issue((t + 1) * KT, (t + 1) & 1);
     do_tile(t, std::false_type{});
-    if (t + 1 < ntiles) store((t & 1) ^ 1);
-    __syncthreads();
   }
   if (nfull < ntiles) {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     do_tile(nfull, std::true_type{});
-    __syncthreads();
   }
+  __syncthreads();
   // ---- normalise and store: stage the wave's 32 x 64 output through LDS so each
   // query row leaves as whole 128-B lines
   const float inv = 1.f / osum[0];
-  u16* stg = (u16*)&sk[0][0] + wave * 32 * KS;   // 32 rows x KS (padded) per wave
+  u16* stg = (u16*)&smem[0][0] + wave * 32 * KS;   // 32 rows x KS (padded) per wave (18 KiB of 32)
   #pragma unroll
   for (int db = 0; db < 2; ++db)
     #pragma unroll
