@@ -71,11 +71,24 @@ int num_cus() {
   }
   return g_num_cu;
 }
+// Fewer tiles than CUs (the decoder's 48^2 - 192^2 convs: 9 - 144 tiles of 256 x 256,
+// 36 - 144 k-steps): the K range of every tile is split over up to SK_MAX_SPLIT
+// workgroups of >= SK_MIN_STEPS k-steps each (the owner adds the others' fp32
+// partials, 256 KiB apiece), or, at more than half a chip of tiles, spread over
+// every CU.  debug flag 32 restores one workgroup per tile.
+constexpr int SK_MIN_STEPS = 8, SK_MAX_SPLIT = 6;
 int sk_grid(const GemmP& p) {
   const int tiles = p.tiles_m * p.tiles_n;
   int g = num_cus();
   if (g > 256) g = 256;   // == SK_MAX_WG (workspace slots)
-  return tiles < g ? tiles : g;
+  if (tiles >= g) return g;
+  if (g_dbg_flags & 32) return tiles;
+  const int kt = p.K / 64;
+  int s = g / tiles;
+  if (s < 2) return kt >= 2 * SK_MIN_STEPS ? g : tiles;
+  if (s > SK_MAX_SPLIT) s = SK_MAX_SPLIT;
+  if (s > kt / SK_MIN_STEPS) s = kt / SK_MIN_STEPS;
+  return tiles * (s < 1 ? 1 : s);
 }
 
 #ifdef DP_STAMPS
@@ -1547,7 +1560,17 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     else if (a->N % 8 != 0) tile = DP_TILE_128x128;
     else if (a->N == 128 && a->M >= 512 * 256) tile = DP_TILE_BIG_512x128;   // N = 128 convs at 768^2
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
-    else if (ws_ok && a->K <= 256 && tiles256 >= 1024) {
+    else if (ws_ok && a->a_mode == DP_A_CONV && !(g_dbg_flags & 32) && tiles256 < num_cus() &&
+             a->K >= 4608) {
+      // Implicit convs with fewer 256 x 256 tiles than CUs and K >= 4608 (the decoder's
+      // 512/1024-channel projections at 48^2 - 192^2) on the stream-K engine, each
+      // tile's K range split (sk_grid): 153 -> 108, 152 -> 112, 152 -> 126 us in-frame
+      // (tools/frame_shapes.py; debug flag 32 = off).  Measured and rejected: the split
+      // at K = 2304 (48^2: 50 -> 80 us), and stream-K for the 384^2 / 768^2 ResidualBlock
+      // convs (ReLU prologue + residual epilogue): 199 -> 265 and 744 -> 970 us in-frame,
+      // although a bias-only conv of the same shape gains 8 % (tools/gemm_bench.py).
+      tile = DP_TILE_STREAMK_256x256;
+    } else if (ws_ok && a->K <= 256 && tiles256 >= 1024) {
       // short-K, many tiles (the 384^2 -> 768^2 deconvs: 4 K steps per tile): the
       // persistent stream-K engine keeps the next tile's loads in flight under each
       // epilogue, which otherwise dominates (tools/gemm_bench.py: 162 vs 198 us)

@@ -7,7 +7,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
 from depth_pro import ops  # noqa: E402
-from depth_pro._lib import (DP_TILE_128x128, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa
+from depth_pro._lib import (DP_TILE_128x128, DP_TILE_256x64, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa
                             DP_TILE_BIG_256x128_K32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32,
                             DP_TILE_DEEP4_256x256, DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128,
                             DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_512x128)
@@ -16,7 +16,7 @@ TILES = (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128
          ("8ph256x256", DP_TILE_8PH_256x256), ("deep4_256x256", DP_TILE_DEEP4_256x256),
          ("deep5_256x256", DP_TILE_DEEP5_256x256), ("deep6_256x128", DP_TILE_DEEP_256x128),
          ("sk256x256", DP_TILE_STREAMK_256x256), ("big320x256", DP_TILE_BIG_320x256),
-         ("small128x128", DP_TILE_128x128), ("big512x128", DP_TILE_BIG_512x128))
+         ("small128x128", DP_TILE_128x128), ("big512x128", DP_TILE_BIG_512x128), ("small256x64", DP_TILE_256x64))
 N256 = (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
         DP_TILE_DEEP5_256x256, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256)
 
@@ -27,6 +27,9 @@ SHAPES = [  # (name, M, N, K, kw)
     ("fc2+res", 20195, 1024, 4096, {"acc": True}),
     ("conv3x3 768^2 256->256", 768 * 768, 256, 2304, {"conv": 768}),
     ("conv3x3 384^2 256->256", 384 * 384, 256, 2304, {"conv": 384}),
+    ("conv3x3 192^2 256->256", 192 * 192, 256, 2304, {"conv": 192}),
+    ("conv3x3 96^2 256->256", 96 * 96, 256, 2304, {"conv": 96}),
+    ("conv3x3 48^2 256->256", 48 * 48, 256, 2304, {"conv": 48}),
     ("head conv 768^2 256->128", 768 * 768, 128, 2304, {"conv": 768}),
     ("composed head 768^2 128->4x32", 768 * 768, 128, 1152, {"conv": 768}),
     ("deconv 384->768 256ch", 384 * 384, 1024, 256, {"deconv": (384, 384, 256)}),
