@@ -7,12 +7,16 @@
 namespace {
 
 // ------------------------------------------------------------------ LayerNorm
-// One wave64 per row, the row held in registers (VEC float4 per lane), two-pass
-// mean / variance in fp32 (timm nn.LayerNorm(eps=1e-6)), 16-bit output.
+// One wave64 per row, the row held in registers, two-pass mean / variance in
+// fp32 (timm nn.LayerNorm(eps=1e-6)), 16-bit output.  Lane l owns the 8
+// consecutive columns 8 l + 512 j (j < VEC / 2): two 16-B loads per group and ONE
+// 16-B store (a full 1 KiB line set per wave-instruction; 8-B stores wrote half).
 template <typename K_, int VEC>
 __global__ void __launch_bounds__(256) ln_kernel(const float* __restrict__ x, long long ldx,
                                                  const float* __restrict__ w, const float* __restrict__ b,
                                                  u16* __restrict__ y, long long ldy, int rows, float eps) {
+  static_assert(VEC % 2 == 0, "8 columns per lane");
+  constexpr int G = VEC / 2;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -21,10 +25,12 @@ __global__ void __launch_bounds__(256) ln_kernel(const float* __restrict__ x, lo
   float4 v[VEC];
   float s = 0.f;
   #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    v[i] = *(const float4*)(xr + i * 256 + lane * 4);
-    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  for (int j = 0; j < G; ++j) {
+    v[2 * j] = *(const float4*)(xr + j * 512 + lane * 8);
+    v[2 * j + 1] = *(const float4*)(xr + j * 512 + lane * 8 + 4);
   }
+  #pragma unroll
+  for (int i = 0; i < VEC; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
   #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   const float mean = s * (1.f / COLS);
@@ -39,19 +45,49 @@ __global__ void __launch_bounds__(256) ln_kernel(const float* __restrict__ x, lo
   const float rstd = rsqrtf(q * (1.f / COLS) + eps);
   u16* yr = y + (long long)row * ldy;
   #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    const int c0 = i * 256 + lane * 4;
-    float4 g = *(const float4*)(w + c0);
-    float4 bb = *(const float4*)(b + c0);
-    float o0 = (v[i].x - mean) * rstd * g.x + bb.x;
-    float o1 = (v[i].y - mean) * rstd * g.y + bb.y;
-    float o2 = (v[i].z - mean) * rstd * g.z + bb.z;
-    float o3 = (v[i].w - mean) * rstd * g.w + bb.w;
-    uint2 pk;
-    pk.x = (uint32_t)K_::from_f(o0) | ((uint32_t)K_::from_f(o1) << 16);
-    pk.y = (uint32_t)K_::from_f(o2) | ((uint32_t)K_::from_f(o3) << 16);
-    *(uint2*)(yr + c0) = pk;
+  for (int j = 0; j < G; ++j) {
+    const int c0 = j * 512 + lane * 8;
+    uint32_t pk[4];
+    #pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4 g = *(const float4*)(w + c0 + 4 * h);
+      const float4 bb = *(const float4*)(b + c0 + 4 * h);
+      const float4 t = v[2 * j + h];
+      const float o0 = (t.x - mean) * rstd * g.x + bb.x;
+      const float o1 = (t.y - mean) * rstd * g.y + bb.y;
+      const float o2 = (t.z - mean) * rstd * g.z + bb.z;
+      const float o3 = (t.w - mean) * rstd * g.w + bb.w;
+      pk[2 * h] = (uint32_t)K_::from_f(o0) | ((uint32_t)K_::from_f(o1) << 16);
+      pk[2 * h + 1] = (uint32_t)K_::from_f(o2) | ((uint32_t)K_::from_f(o3) << 16);
+    }
+    *(uint4*)(yr + c0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
   }
+}
+
+// 256 columns: one float4 per lane, 8-B stores
+template <typename K_>
+__global__ void __launch_bounds__(256) ln256_kernel(const float* __restrict__ x, long long ldx,
+                                                    const float* __restrict__ w, const float* __restrict__ b,
+                                                    u16* __restrict__ y, long long ldy, int rows, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float4 v = *(const float4*)(x + (long long)row * ldx + lane * 4);
+  float s = (v.x + v.y) + (v.z + v.w);
+  #pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s * (1.f / 256);
+  const float a = v.x - mean, bb = v.y - mean, c = v.z - mean, d = v.w - mean;
+  float q = (a * a + bb * bb) + (c * c + d * d);
+  #pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = rsqrtf(q * (1.f / 256) + eps);
+  const float4 g = *(const float4*)(w + lane * 4);
+  const float4 bv = *(const float4*)(b + lane * 4);
+  uint2 pk;
+  pk.x = (uint32_t)K_::from_f(a * rstd * g.x + bv.x) | ((uint32_t)K_::from_f(bb * rstd * g.y + bv.y) << 16);
+  pk.y = (uint32_t)K_::from_f(c * rstd * g.z + bv.z) | ((uint32_t)K_::from_f(d * rstd * g.w + bv.w) << 16);
+  *(uint2*)(y + (long long)row * ldy + lane * 4) = pk;
 }
 
 template <typename K_>
@@ -59,7 +95,7 @@ int ln_launch(const float* x, long long ldx, const float* w, const float* b, u16
               int rows, int cols, float eps, hipStream_t s) {
   dim3 grid((rows + 3) / 4);
   switch (cols) {
-    case 256: hipLaunchKernelGGL((ln_kernel<K_, 1>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
+    case 256: hipLaunchKernelGGL((ln256_kernel<K_>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
     case 512: hipLaunchKernelGGL((ln_kernel<K_, 2>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
     case 1024: hipLaunchKernelGGL((ln_kernel<K_, 4>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
     case 2048: hipLaunchKernelGGL((ln_kernel<K_, 8>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
@@ -290,6 +326,7 @@ extern "C" int dp_layernorm(const float* x, int64_t ldx, const float* w, const f
                             int32_t rows, int32_t cols, float eps, int32_t dtype, dp_stream_t stream) {
   if (!x || !w || !b || !y) return DP_ERR_ARG;
   if (rows <= 0 || ldx % 4 || ldy % 4) return DP_ERR_SHAPE;
+  if (cols > 256 && (ldy % 8 || (uintptr_t)y % 16)) return DP_ERR_ALIGN;   // 16-B row stores
   hipStream_t s = (hipStream_t)stream;
   if (dtype == DP_BF16) return ln_launch<KBF16>(x, ldx, w, b, (u16*)y, ldy, rows, cols, eps, s);
   if (dtype == DP_F16) return ln_launch<KF16>(x, ldx, w, b, (u16*)y, ldy, rows, cols, eps, s);

@@ -153,14 +153,15 @@ def test_attention(cuda, dt, batch, seq):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-def test_layernorm(cuda, dt):
-    g = torch.Generator().manual_seed(17)
-    x = (torch.randn(1234, 1024, generator=g) * 3 + 1).to(cuda)
-    w = torch.randn(1024, generator=g).to(cuda)
-    b = torch.randn(1024, generator=g).to(cuda)
-    y = torch.empty(1234, 1024, dtype=dt, device=cuda)
-    ops.layernorm(x, w, b, y, 1234, 1024)
-    close(y, F.layer_norm(x, (1024,), w, b, 1e-6), dt, "layernorm")
+@pytest.mark.parametrize("cols", [1024, 256, 512, 2048])
+def test_layernorm(cuda, dt, cols):
+    g = torch.Generator().manual_seed(17 + cols)
+    x = (torch.randn(1234, cols, generator=g) * 3 + 1).to(cuda)
+    w = torch.randn(cols, generator=g).to(cuda)
+    b = torch.randn(cols, generator=g).to(cuda)
+    y = torch.empty(1234, cols, dtype=dt, device=cuda)
+    ops.layernorm(x, w, b, y, 1234, cols)
+    close(y, F.layer_norm(x, (cols,), w, b, 1e-6), dt, "layernorm")
 
 
 @pytest.mark.parametrize("dt", DTYPES)
