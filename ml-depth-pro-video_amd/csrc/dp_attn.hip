@@ -85,6 +85,10 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     qf[ks] = make_uint4(0, 0, 0, 0);
     if (q < seq) qf[ks] = *(const uint4*)(base + (long long)q * ldq + qcol + 16 * ks + 8 * hi);
   }
+  // Q has landed (a wait the compiler sees): otherwise its own vmcnt(0) for Q's
+  // first use lands inside the tile loop, where it also waits for the next tile's
+  // LDS-DMA (inline asm, invisible to it) and serialises that latency every tile.
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
 
   // LDS-DMA staging: piece i of wave w fills key rows 32 i + 8 w + lane / 8, slot
   // lane % 8 of each 128-B row; the slot holds logical chunk slot ^ swizzle(row), so
