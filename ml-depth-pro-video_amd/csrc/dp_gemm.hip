@@ -1594,6 +1594,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       const long long cost256 = (tiles256 + ncu - 1) / ncu * 256 * 20, cost320 = (tiles320 + ncu - 1) / ncu * 320 * 20;
       const long long cost128 = (tiles128 + ncu - 1) / ncu * 128 * 23;
       if (cost128 < cost256 && cost128 < cost320) tile = DP_TILE_BIG_256x128;
+      // ties (fc1: 4 rounds of 320 rows = 5 of 256) stay on the 8-phase engine: the
+      // 320 x 256 engine is 6 % faster on fc1 in isolation (205 vs 217 us) but equal
+      // in-frame (199-203 us both, profiles/r01s_fc1_engine_ab/)
       else if (cost320 < cost256) tile = DP_TILE_BIG_320x256;
       else tile = (tiles256 >= 600 && a->a_mode != DP_A_CONV) ? DP_TILE_8PH_256x256 : DP_TILE_BIG_256x256;
     }

@@ -86,3 +86,15 @@ def test_gemm_plan_tile_choice():
     ws = lib.dp_gemm_workspace_size()
     rc, tile, wgs = plan(20195, 3072, 1024, tile=_lib.DP_TILE_STREAMK_256x256, workspace=256, workspace_bytes=ws)
     assert rc == 0 and tile == _lib.DP_TILE_STREAMK_256x256 and 1 <= wgs <= 256
+
+    # decoder 3x3 convs: long-K projections with < 1 tile per CU go to stream-K with
+    # split K ranges (needs a workspace); K = 2304 small grids stay data-parallel
+    def conv(S, cin, **kw):
+        return plan(S * S, 256, 9 * cin, a_mode=_lib.DP_A_CONV, in_h=S, in_w=S, in_c=cin, k_h=3, k_w=3,
+                    stride=1, pad=1, out_h=S, out_w=S, **kw)
+    wsk = dict(workspace=256, workspace_bytes=ws)
+    assert conv(48, 1024, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 9 * 6)     # 9 tiles x split 6
+    assert conv(96, 1024, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 36 * 6)    # 36 tiles x split 6
+    assert conv(192, 512, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 256)       # 144 tiles over 256 CUs
+    assert conv(48, 1024)[1] != _lib.DP_TILE_STREAMK_256x256                        # no workspace
+    assert conv(48, 256, **wsk)[1] == _lib.DP_TILE_BIG_256x128                     # K = 2304
