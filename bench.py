@@ -33,9 +33,15 @@ PEAK_HBM_GBS = 8000.0
 
 TILE_NAMES = {1: "128x128", 2: "256x64", 3: "256x32", 4: "256x256", 5: "256x128", 8: "8phase-256x256",
               12: "streamK-256x256", 13: "320x256", 14: "512x128"}
-TILE_KERNEL = {1: "gemm_kernel<KBF16, 128, 128", 4: "gemm_big_kernel<KBF16, 256, 256", 5: "gemm_big_kernel<KBF16, 256, 128",
-               8: "gemm_8ph_kernel<KBF16", 12: "gemm_sk_kernel<KBF16", 13: "gemm_big_kernel<KBF16, 320, 256",
-               14: "gemm_big_kernel<KBF16, 512, 128"}
+TILE_KERNEL = {1: "gemm_kernel<{K}, 128, 128", 4: "gemm_big_kernel<{K}, 256, 256", 5: "gemm_big_kernel<{K}, 256, 128",
+               8: "gemm_8ph_kernel<{K}", 12: "gemm_sk_kernel<{K}", 13: "gemm_big_kernel<{K}, 320, 256",
+               14: "gemm_big_kernel<{K}, 512, 128"}
+
+
+def tile_kernel(tile: int, dtype: torch.dtype) -> str:
+    """Kernel-name prefix (as rocprofv3 prints it) of the GEMM engine `tile` for operand type `dtype`."""
+    t = TILE_KERNEL.get(tile)
+    return t.format(K="KBF16" if dtype == torch.bfloat16 else "KF16") if t else ""
 
 
 def pmc_traffic(kernel: str, workgroups: int):
@@ -87,8 +93,25 @@ def depth_parity(depth: torch.Tensor, canonical: torch.Tensor, fov: torch.Tensor
             "reference": "tests/golden/golden_forward_frame0.npz"}
 
 
-def cpu_baseline(seconds_cap: float = 60.0) -> dict:
-    """The fp32 CPU oracle (a port of the reference path) on one synthetic frame."""
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline() -> dict:
+    """The fp32 CPU oracle (a port of the reference path) on one synthetic frame.
+
+    Bounded sample (~20 s on 16 host threads): one untimed warm-up of a ViT block at
+    the patch-encoder shape's first window (thread pool + allocator), then one timed
+    frame through the oracle's `infer` (a full frame takes ~20 s, so a median of 3 would
+    push the default bench past its time budget; the box-to-box spread is reported
+    in DESIGN.md instead).
+    """
     from depth_pro.weights import synthetic_state_dict
     from oracle import depth_pro_oracle as O
 
@@ -96,12 +119,16 @@ def cpu_baseline(seconds_cap: float = 60.0) -> dict:
     torch.set_num_threads(threads)
     sd = synthetic_state_dict(0)
     x = O.transform(frame(0))
+    with torch.no_grad():
+        O.vit_block(sd, "encoder.patch_encoder.blocks.0.", torch.zeros(1, 577, 1024))
     t0 = time.time()
     with torch.no_grad():
         O.infer(sd, x)
     dt = time.time() - t0
     return {"value": 1.0 / dt, "unit": "frames/sec", "cores": threads, "kind": "port",
-            "sample": f"1 synthetic 1536x1536 frame through oracle/depth_pro_oracle.infer (fp32 torch CPU), {dt:.1f} s"}
+            "cpu_model": cpu_model(),
+            "sample": f"1 synthetic 1536x1536 frame through oracle/depth_pro_oracle.infer (fp32 torch CPU, "
+                      f"after a 1-block warm-up), {dt:.1f} s"}
 
 
 def main():
@@ -109,7 +136,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--dtype", choices=["bf16", "fp16"], default="bf16")
+    ap.add_argument("--dtype", choices=["bf16", "fp16", "mixed"], default="bf16",
+                    help="compute precision: bf16 / fp16 everywhere, or mixed = bf16 ViTs + f16 maps, "
+                         "decoder and heads (depth_pro.depth_pro.PRECISION_MODES)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct resident frames per rank")
@@ -209,8 +238,8 @@ def main():
         eng.forward()
         rec = ops.profile_end()
         eng.serial_side = False
-        for kind, flops, shape, ms in rec:
-            k = groups.setdefault((kind, shape), {"launches": 0, "ms": 0.0, "flop": 0.0})
+        for kind, flops, shape, kdt, ms in rec:
+            k = groups.setdefault((kind, shape, kdt), {"launches": 0, "ms": 0.0, "flop": 0.0})
             k["launches"] += 1
             k["ms"] += ms
             k["flop"] += flops
@@ -226,7 +255,7 @@ def main():
     if rank == 0:
         achieved = fps_per_gpu * FLOP_PER_FRAME / 1e12
         kern = {}
-        for (kind, shape), g in groups.items():
+        for (kind, shape, _), g in groups.items():
             k = kern.setdefault(kind, {"launches": 0, "ms": 0.0, "flop": 0.0})
             for f in ("launches", "ms", "flop"):
                 k[f] += g[f]
@@ -238,17 +267,19 @@ def main():
         dom_avg_us = 1000.0 * dom["ms"] / dom["launches"]
         dom_flop = dom["flop"] / dom["launches"]
         dom_tf = dom_flop / (dom_avg_us * 1e-6) / 1e12
-        dom_info = {"kind": dom_key[0], "shape": list(dom_key[1]), "launches_per_frame": dom["launches"],
+        dom_info = {"kind": dom_key[0], "shape": list(dom_key[1]), "dtype": str(dom_key[2]).replace("torch.", ""),
+                    "launches_per_frame": dom["launches"],
                     "avg_us": round(dom_avg_us, 2), "flop_per_launch": dom_flop,
                     "share_of_frame_kernel_time": round(dom["ms"] / sum(g["ms"] for g in groups.values()), 3)}
         traffic = None
         if dom_key[0].startswith("gemm"):
             M, N, K = dom_key[1]
-            A = torch.empty(8, dtype=eng.dt, device=dev)
+            kdt = dom_key[2]
+            A = torch.empty(8, dtype=kdt, device=dev)
             tile, wgs = ops.gemm(A, A, A, M=M, N=N, K=K, plan_only=True, workspace=eng.ws_main)
             dom_info["engine"] = {"tile": TILE_NAMES.get(tile, tile), "workgroups": wgs,
-                                  "kernel": TILE_KERNEL.get(tile, "")}
-            traffic = pmc_traffic(TILE_KERNEL.get(tile, "?"), wgs)
+                                  "kernel": tile_kernel(tile, kdt)}
+            traffic = pmc_traffic(tile_kernel(tile, kdt), wgs) if tile_kernel(tile, kdt) else None
             if traffic is not None:
                 dom_info["traffic_source"] = traffic.pop("source")
         out = {
@@ -262,7 +293,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.dtype,
+            "dtype": {"bf16": "bf16", "fp16": "f16", "mixed": "bf16+f16"}[args.dtype],
             "data": "synthetic (uint8 1536x1536 frames from numpy default_rng(k); synthetic seed-0 weights, "
                     "full Depth Pro architecture, 951,991,330 params)",
             "config": {"workload": "BASELINE config 2/3: one 1536x1536 frame per GPU per step through "

@@ -17,7 +17,11 @@
  *     before anything was launched;
  *   - 16-bit tensors are raw bits (uint16) whose kind is given by a DP_BF16 /
  *     DP_F16 dtype argument; fp32 tensors are `float`.
- *   - thread-safe for concurrent calls on distinct streams (no global state).
+ *   - safe for concurrent calls from several host threads on distinct streams: the
+ *     library's only process-wide state is a per-device CU-count cache (written once,
+ *     same value from every writer) and the debug/fault-injection word of the
+ *     tools-only `dp_gemm_debug_flags` (not declared here), which must not change
+ *     while other threads launch.
  */
 #ifndef DP_MI355X_H
 #define DP_MI355X_H
@@ -125,9 +129,16 @@ int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 
 /*
  * Bytes of workspace the stream-K engine needs (flags + one fp32 256x256 partial
- * tile per persistent workgroup).  Zeroed by dp_gemm itself (a memset node on
- * the same stream) before each stream-K launch; contents are scratch.
+ * tile per persistent workgroup).  The caller zeroes it once after allocation; its
+ * hand-off flags are cleared by dp_gemm itself (a memset node on the same stream)
+ * before each stream-K launch, the rest is scratch -- except the ERROR WORD: the
+ * uint32 at byte offset DP_GEMM_WS_ERROR_OFFSET becomes non-zero when a stream-K
+ * launch on this workspace gave up waiting for another workgroup's partial tile
+ * (bounded spin; the output of that launch is then wrong).  It is sticky: nothing
+ * but the caller clears it, so one read after a whole forward / graph replay covers
+ * every launch in it.
  */
+#define DP_GEMM_WS_ERROR_OFFSET 4092
 int64_t dp_gemm_workspace_size(void);
 
 /*

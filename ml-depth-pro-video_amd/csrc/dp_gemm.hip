@@ -20,6 +20,8 @@
 // A-operand and the activation fragment as B, so D = C^T: each lane ends up
 // with 4 consecutive output channels of one output row, and bias / gamma /
 // residual loads and the stores are 8-16 B per lane.
+#include <atomic>
+
 #include "dp_common.h"
 
 namespace {
@@ -58,18 +60,24 @@ struct GemmP {
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
 };
 
-int g_dbg_flags = 0;
+// Process-wide ablation / fault-injection bits, set only by dp_gemm_debug_flags (tools and
+// tests; not in the ABI header).  Read once per dp_gemm call.
+std::atomic<int> g_dbg_flags{0};
 
-// persistent workgroups of the stream-K engine: one per CU, at most one per tile
-int g_num_cu = 0;
+// persistent workgroups of the stream-K engine: one per CU, at most one per tile.
+// CU count per device, cached (benign race: every writer stores the same value).
+constexpr int DP_MAX_DEV = 64;
+std::atomic<int> g_num_cu[DP_MAX_DEV];
 int num_cus() {
-  if (g_num_cu == 0) {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    g_num_cu = n;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  std::atomic<int>& slot = g_num_cu[dev < DP_MAX_DEV ? dev : 0];
+  int n = slot.load(std::memory_order_relaxed);
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    if (dev < DP_MAX_DEV) slot.store(n, std::memory_order_relaxed);
   }
-  return g_num_cu;
+  return n;
 }
 // Fewer tiles than CUs (the decoder's 48^2 - 192^2 convs: 9 - 144 tiles of 256 x 256,
 // 36 - 144 k-steps): the K range of every tile is split over up to SK_MAX_SPLIT
@@ -82,7 +90,7 @@ int sk_grid(const GemmP& p) {
   int g = num_cus();
   if (g > 256) g = 256;   // == SK_MAX_WG (workspace slots)
   if (tiles >= g) return g;
-  if (g_dbg_flags & 32) return tiles;
+  if (p.dbg & 32) return tiles;
   const int kt = p.K / 64;
   int s = g / tiles;
   if (s < 2) return kt >= 2 * SK_MIN_STEPS ? g : tiles;
@@ -1053,7 +1061,9 @@ constexpr int SK_STAGE = 2 * SK_A_BYTES;         // A + B
 constexpr int SK_RING = 2 * SK_STAGE;            // 2 stages: 128 KiB
 constexpr int SK_EPI = 8 * 16 * 64 * 4;          // 8 waves x 16 rows x 64 fp32
 constexpr int SK_TILE_F = 256 * 256;             // floats per partial slot
-constexpr long long SK_FLAG_BYTES = 4096;        // flags [0, G), error word at [1023]
+constexpr long long SK_FLAG_BYTES = 4096;        // flags [0, G) (cleared per launch), error word at [1023] (sticky)
+constexpr long long SK_CLEAR_BYTES = 4 * 256;     // the per-launch memset: flags only
+static_assert(DP_GEMM_WS_ERROR_OFFSET == 4 * 1023, "error word offset (dp_mi355x.h)");
 constexpr int SK_MAX_WG = 256;
 
 struct SkP {
@@ -1232,9 +1242,11 @@ __global__ void __launch_bounds__(512, 1) gemm_sk_kernel(const GemmP p, const Sk
   auto absorb = [&](int q) {   // add workgroup q's published partial of the tile
     if (tid == 0) {
       unsigned spins = 0;
-      while (__hip_atomic_load(s.flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      // debug bit 64 (tests only): give up at once, as a starved wait would
+      const unsigned limit = (p.dbg & 64) ? 0u : (1u << 24);
+      while (__hip_atomic_load(s.flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u || (p.dbg & 64)) {
         __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) {  // ~seconds: never hang the GPU; report instead
+        if (++spins > limit) {  // ~seconds: never hang the GPU; report in the sticky error word instead
           __hip_atomic_store(s.flags + 1023, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
@@ -1293,7 +1305,7 @@ int launch_sk(const GemmP& p0, bool conv, void* ws, hipStream_t st) {
   const int G = sk_grid(p);
   s.flags = (uint32_t*)ws;
   s.part = (float*)((char*)ws + SK_FLAG_BYTES);
-  hipError_t e = hipMemsetAsync(ws, 0, SK_FLAG_BYTES, st);
+  hipError_t e = hipMemsetAsync(ws, 0, SK_CLEAR_BYTES, st);
   if (e != hipSuccess) return (int)e;
   dim3 grid(G);
   const bool rowld = p.R1 || p.R2 || p.pos || p.accumulate;
@@ -1515,7 +1527,7 @@ extern "C" int dp_gemm_stamps(void* host_dst, int n_wg) {
 
 // Not part of the ABI header: ablation switches for the GEMM microbenchmark only.
 extern "C" int dp_gemm_debug_flags(int flags) {
-  g_dbg_flags = flags;
+  g_dbg_flags.store(flags, std::memory_order_relaxed);
   return 0;
 }
 
@@ -1550,6 +1562,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       return DP_ERR_SHAPE;
   }
   const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
+  const int dbg = g_dbg_flags.load(std::memory_order_relaxed);
   tile = a->tile;
   if (a->store_mode == DP_STORE_HEAD_PS) {
     // 32-column parity groups must not straddle a wave's columns (TN = 32 or 64)
@@ -1566,7 +1579,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     else if (a->N % 8 != 0) tile = DP_TILE_128x128;
     else if (a->N == 128 && a->M >= 512 * 256) tile = DP_TILE_BIG_512x128;   // N = 128 convs at 768^2
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
-    else if (ws_ok && a->a_mode == DP_A_CONV && !(g_dbg_flags & 32) && tiles256 < num_cus() &&
+    else if (ws_ok && a->a_mode == DP_A_CONV && !(dbg & 32) && tiles256 < num_cus() &&
              a->K >= 4608) {
       // Implicit convs with fewer 256 x 256 tiles than CUs and K >= 4608 (the decoder's
       // 512/1024-channel projections at 48^2 - 192^2) on the stream-K engine, each
@@ -1622,7 +1635,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     p.tiles_n = a->N / 256;
     p.tiles_m = (a->M + 255) / 256;
   }
-  p.dbg = g_dbg_flags;
+  p.dbg = dbg;
   return 0;
 }
 }  // namespace

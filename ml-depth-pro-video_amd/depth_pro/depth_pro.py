@@ -63,13 +63,20 @@ def _check_preset(preset: ViTPreset) -> None:
         raise KeyError(f"Preset {preset} not found.")  # depth_pro.py:67
 
 
-def _compute_dtype(precision: torch.dtype) -> int:
+# DEPTH_PRO_COMPUTE_DTYPE values -> (ViT operand type, decoder/head operand type)
+PRECISION_MODES = {"bf16": (DP_BF16, DP_BF16), "fp16": (DP_F16, DP_F16), "mixed": (DP_BF16, DP_F16)}
+
+
+def _compute_dtype(precision: torch.dtype) -> Tuple[int, int]:
+    """(ViT code, decoder code) for `precision` (or the DEPTH_PRO_COMPUTE_DTYPE override)."""
     env = os.environ.get("DEPTH_PRO_COMPUTE_DTYPE", "").lower()
-    if env in ("fp16", "f16", "half", "float16"):
-        return DP_F16
-    if env in ("bf16", "bfloat16"):
-        return DP_BF16
-    return DP_F16 if precision == torch.half else DP_BF16
+    alias = {"f16": "fp16", "half": "fp16", "float16": "fp16", "bfloat16": "bf16", "bf16+f16": "mixed"}
+    env = alias.get(env, env)
+    if env in PRECISION_MODES:
+        return PRECISION_MODES[env]
+    if env:
+        raise ValueError(f"DEPTH_PRO_COMPUTE_DTYPE={env!r}: expected one of {sorted(PRECISION_MODES)}")
+    return PRECISION_MODES["fp16"] if precision == torch.half else PRECISION_MODES["bf16"]
 
 
 class Transform:
@@ -112,7 +119,8 @@ def _module_tree(spec, device, dtype) -> nn.Module:
 class DepthPro(nn.Module):
     """DepthPro network (reference depth_pro.py:154-298) on the MI355X engine."""
 
-    def __init__(self, use_fov_head: bool = True, device=torch.device("cpu"), compute_dtype: int = DP_BF16):
+    def __init__(self, use_fov_head: bool = True, device=torch.device("cpu"),
+                 compute_dtype: Tuple[int, int] = (DP_BF16, DP_BF16)):
         super().__init__()
         tree = _module_tree(param_spec(use_fov_head), device, torch.float32)
         for name, child in tree.named_children():
@@ -189,26 +197,36 @@ class DepthPro(nn.Module):
         f_px: Optional[Union[float, torch.Tensor]] = None,
         interpolation_mode="bilinear",
     ) -> Mapping[str, torch.Tensor]:
-        """Infer depth [m] and focal length [px] (reference depth_pro.py:243-298)."""
+        """Infer depth [m] and focal length [px] (reference depth_pro.py:243-298).
+
+        x: (3,H,W) or (B,3,H,W).  As in the reference, a batch gives depth (B,H,W) and,
+        without a given f_px, one focal length per frame (B,); frames run one at a time
+        through the engine (each a full 1536^2 forward).
+        """
         if interpolation_mode != "bilinear":
             raise NotImplementedError("only interpolation_mode='bilinear' (the reference default) is supported")
         if len(x.shape) == 3:
             x = x.unsqueeze(0)
-        _, _, H, W = x.shape
+        B, _, H, W = x.shape
         eng = self.engine()
-        # prologue: (resize to) 1536^2 fp32 straight into the engine's static input
-        ops.resize_bilinear(x[0], eng.x0)
-        canonical, fov_deg = eng.run()
-        depth = torch.empty(H, W, dtype=torch.float32, device=x.device)
-        if f_px is None:
-            if not self.use_fov_head:
-                raise TypeError("f_px is required when the model has no FOV head")
-            f_out = torch.empty((), dtype=torch.float32, device=x.device)
-            ops.infer_epilogue(canonical, fov_deg, None, H, W, depth, f_out)
-            f_px = f_out
-        else:
+        if f_px is None and not self.use_fov_head:
+            raise TypeError("f_px is required when the model has no FOV head")
+        given = None
+        if f_px is not None:
             given = float(f_px.detach().float().reshape(-1)[0].item()) if torch.is_tensor(f_px) else float(f_px)
-            ops.infer_epilogue(canonical, None, given, H, W, depth, None)
+        depth = torch.empty(B, H, W, dtype=torch.float32, device=x.device)
+        f_out = torch.empty(B, dtype=torch.float32, device=x.device) if f_px is None else None
+        for b in range(B):
+            # prologue: (resize to) 1536^2 fp32 straight into the engine's static input
+            ops.resize_bilinear(x[b], eng.x0)
+            canonical, fov_deg = eng.run()
+            if f_px is None:
+                ops.infer_epilogue(canonical, fov_deg, None, H, W, depth[b], f_out[b])
+            else:
+                ops.infer_epilogue(canonical, None, given, H, W, depth[b], None)
+        if f_px is None:
+            f_px = f_out.squeeze()
+        else:
             f_px = f_px.squeeze()  # mirrors depth_pro.py:286 (a plain Python float has no .squeeze)
         return {"depth": depth.squeeze(), "focallength_px": f_px}
 

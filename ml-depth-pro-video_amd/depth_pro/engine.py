@@ -85,8 +85,28 @@ def compose_head(wd: torch.Tensor, bd: torch.Tensor, w2: torch.Tensor, b2: torch
             "head.ps.corr": corr.reshape(-1).contiguous()}
 
 
-def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: int) -> Dict[str, object]:
+def precision_codes(codes) -> Tuple[int, int]:
+    """(ViT code, decoder code) from one DP_BF16 / DP_F16 code or a pair of them.
+
+    The ViTs (qkv / attention / proj / fc1 / fc2, fp32 residual stream) run in the
+    first type; everything from the final ViT LayerNorm output on -- merged maps,
+    project/upsample, decoder, heads, FOV tail -- in the second.
+    """
+    if isinstance(codes, (tuple, list)):
+        v, d = int(codes[0]), int(codes[1])
+    else:
+        v = d = int(codes)
+    for c in (v, d):
+        if c not in (DP_BF16, DP_F16):
+            raise DPError("compute dtype must be bf16 or f16")
+    return v, d
+
+
+def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code) -> Dict[str, object]:
     """Convert a (reference-named) state dict into GEMM-ready device tensors.
+
+    `dtype_code`: one DP_BF16 / DP_F16 code, or (ViT code, decoder code) -- see
+    `precision_codes`.
 
     Linear weights stay [N][K]; conv weights become [Cout][ky][kx][Cin]; k2s2
     deconvs [(dy,dx,Cout)][Cin].  Each decoder fusion's deconv (no bias) and the
@@ -95,7 +115,8 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: 
     (W'[ci,co] = sum_c Wd[ci,c] Wo[co,c]): the 1x1 pass at the upsampled
     resolution disappears from the frame.
     """
-    dt = ops.torch_dtype(dtype_code)
+    vcode, dcode = precision_codes(dtype_code)
+    vdt, dt = ops.torch_dtype(vcode), ops.torch_dtype(dcode)
     g = lambda k: sd[k].detach().to(device)  # noqa: E731
     P: Dict[str, object] = {}
     for vit in ("encoder.patch_encoder.", "encoder.image_encoder.", "fov.encoder.0."):
@@ -103,7 +124,7 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: 
             continue
         P[vit + "cls"] = _f32(g(vit + "cls_token")).reshape(D)
         P[vit + "pos"] = _f32(g(vit + "pos_embed")).reshape(TOK, D)
-        P[vit + "pe.w"] = g(vit + "patch_embed.proj.weight").reshape(D, -1).to(dt).contiguous()
+        P[vit + "pe.w"] = g(vit + "patch_embed.proj.weight").reshape(D, -1).to(vdt).contiguous()
         P[vit + "pe.b"] = _f32(g(vit + "patch_embed.proj.bias"))
         for i in range(DEPTH):
             b = f"{vit}blocks.{i}."
@@ -111,7 +132,7 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: 
                       "attn.proj.bias", "mlp.fc1.bias", "mlp.fc2.bias", "ls1.gamma", "ls2.gamma"):
                 P[b + n] = _f32(g(b + n))
             for n in ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight"):
-                P[b + n] = g(b + n).to(dt).contiguous()
+                P[b + n] = g(b + n).to(vdt).contiguous()
         P[vit + "norm.weight"] = _f32(g(vit + "norm.weight"))
         P[vit + "norm.bias"] = _f32(g(vit + "norm.bias"))
     # encoder project / upsample
@@ -167,38 +188,44 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code: 
 
 # ---------------------------------------------------------------------- engine
 class _ViTBuffers:
-    def __init__(self, rows: int, dt, dev):
+    def __init__(self, rows: int, dt, dev, out_dt=None):
         self.rows = rows
         self.x = torch.empty(rows, D, dtype=torch.float32, device=dev)
         self.h = torch.empty(rows, D, dtype=dt, device=dev)
         self.qkv = torch.empty(rows, 3 * D, dtype=dt, device=dev)
         self.a = torch.empty(rows, D, dtype=dt, device=dev)
         self.m = torch.empty(rows, MLP_DIM, dtype=dt, device=dev)
+        # final-norm output (the encoder features) in the decoder's type; it reuses the
+        # attention-output buffer, which is dead once the last block has run
+        out_dt = out_dt or dt
+        self.out = self.h if out_dt == dt else self.a.view(out_dt)
 
 
 class Engine:
     """One frame (batch 1) per forward; static workspace (~4 GB)."""
 
-    def __init__(self, packed: Dict[str, object], device: torch.device, dtype_code: int,
+    def __init__(self, packed: Dict[str, object], device: torch.device, dtype_code,
                  use_fov: bool = True):
         load()
         if device.type != "cuda":
             raise DPError("the MI355X Depth Pro engine needs a ROCm/HIP device")
-        if dtype_code not in (DP_BF16, DP_F16):
-            raise DPError("compute dtype must be bf16 or f16")
+        self.vcode, self.code = precision_codes(dtype_code)
+        if packed[next(k for k in packed if k.endswith("attn.qkv.weight"))].dtype != ops.torch_dtype(self.vcode) \
+                or packed["decoder.convs.4"].dtype != ops.torch_dtype(self.code):
+            raise DPError("packed weights were made for another compute precision")
         self.P = packed
         self.dev = device
-        self.code = dtype_code
-        self.dt = ops.torch_dtype(dtype_code)
+        self.vdt = ops.torch_dtype(self.vcode)   # ViT GEMM / attention operands
+        self.dt = ops.torch_dtype(self.code)     # encoder maps, decoder, heads
         self.use_fov = use_fov and "fov.lin.w" in packed
-        dt, dev = self.dt, device
+        dt, vdt, dev = self.dt, self.vdt, device
         e = lambda *s, dtype=None: torch.empty(*s, dtype=dtype or dt, device=dev)  # noqa: E731
         S = IMG_SIZE
         self.x0 = e(3, S, S, dtype=torch.float32)           # network input (normalized, 1536^2)
-        self.cols = e(NWIN * PTOK, 768)
-        self.vp = _ViTBuffers(NWIN * TOK, dt, dev)          # patch encoder (35 windows)
-        self.vi = _ViTBuffers(TOK, dt, dev)                 # image encoder
-        self.vf = _ViTBuffers(TOK, dt, dev) if self.use_fov else None
+        self.cols = e(NWIN * PTOK, 768, dtype=vdt)
+        self.vp = _ViTBuffers(NWIN * TOK, vdt, dev, dt)     # patch encoder (35 windows)
+        self.vi = _ViTBuffers(TOK, vdt, dev, dt)            # image encoder
+        self.vf = _ViTBuffers(TOK, vdt, dev, dt) if self.use_fov else None
         # merged encoder maps (NHWC)
         self.lat0 = e(96 * 96, D)
         self.lat1 = e(96 * 96, D)
@@ -242,6 +269,13 @@ class Engine:
         # stream-K GEMM scratch, one per stream that issues GEMMs (main / side)
         self.ws_main = ops.gemm_workspace(dev)
         self.ws_side = ops.gemm_workspace(dev)
+        # their sticky error words (dp_mi355x.h DP_GEMM_WS_ERROR_OFFSET), read back asynchronously
+        # after every forward into pinned memory and checked by `check_status`
+        self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32)
+                         for w in (self.ws_main, self.ws_side)]
+        self._err_host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        self._err_ev: Optional[torch.cuda.Event] = None
+        self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
         self.serial_side = False   # True: run the side encoders on the current stream (profiling)
         # FOV encoder + head beside the decoder instead of the patch encoder (measured: 0.3 ms
         # slower on MI355X, so off by default; DP_FOV_LATE=1 to try)
@@ -275,7 +309,7 @@ class Engine:
                          gamma=P[b + "ls2.gamma"], accumulate=True)
             if hooks and i in hooks:
                 hooks[i]()
-        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.h, M, D)
+        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
@@ -320,7 +354,7 @@ class Engine:
         beside the patch encoder."""
         P, e = self.P, "encoder."
         self._vit("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
-        ops.merge_windows(self.vi.h, 0, 1, 0, self.g)
+        ops.merge_windows(self.vi.out, 0, 1, 0, self.g)
         self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
                      C_off=D, ldc=2 * D)
 
@@ -328,7 +362,7 @@ class Engine:
         """FOV encoder ViT + Linear (fov.py:45-47, 66-72)."""
         vf, P = self.vf, self.P
         self._vit("fov.encoder.0.", vf, 1, 34 * PTOK)
-        ops.gemm(vf.h, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
+        ops.gemm(vf.out, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
 
     def _fov_head(self):
         """FOV head (fov.py:56-82): needs the low-res decoder features and the FOV tokens."""
@@ -375,9 +409,9 @@ class Engine:
             11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
         }
         self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks)
-        ops.merge_windows(vp.h, 0, 5, 3, self.f0)
-        ops.merge_windows(vp.h, 25, 3, 6, self.f1)
-        ops.merge_windows(vp.h, 34, 1, 0, self.f2)
+        ops.merge_windows(vp.out, 0, 5, 3, self.f0)
+        ops.merge_windows(vp.out, 25, 3, 6, self.f1)
+        ops.merge_windows(vp.out, 34, 1, 0, self.f2)
         # project / upsample (encoder.py:314-324)
         e = "encoder."
         ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
@@ -442,7 +476,39 @@ class Engine:
         self.graph = g
 
     def run(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """One forward (graph replay if captured).  Raises DPError if an EARLIER forward's
+        stream-K hand-off timed out (or this one's, with DP_CHECK_SYNC=1)."""
+        self.check_status(block=False)
         if self.graph is not None:
             self.graph.replay()
-            return self.canonical, self.fov_deg
-        return self.forward()
+        else:
+            self.forward()
+        self._stage_status()
+        if self.sync_check:
+            self.check_status(block=True)
+        return self.canonical, self.fov_deg
+
+    def _stage_status(self) -> None:
+        for i, w in enumerate(self._err_dev):
+            self._err_host[i:i + 1].copy_(w, non_blocking=True)
+        self._err_ev = torch.cuda.Event()
+        self._err_ev.record()
+
+    def check_status(self, block: bool = True) -> None:
+        """Raise DPError if a stream-K GEMM of a forward run so far gave up waiting for a
+        partial tile (its output -- that frame's depth -- is wrong).  block=False only looks
+        at read-backs that have already landed (no synchronisation)."""
+        ev = self._err_ev
+        if ev is None:
+            return
+        if block:
+            ev.synchronize()
+        elif not ev.query():
+            return
+        self._err_ev = None
+        if int(self._err_host.abs().sum()) != 0:
+            self._err_host.zero_()
+            for w in self._err_dev:
+                w.zero_()
+            raise DPError("dp_gemm stream-K: a partial-tile hand-off timed out; the depth map of a recent "
+                          "frame is invalid (workspace error word set)")

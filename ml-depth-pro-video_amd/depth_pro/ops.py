@@ -30,7 +30,7 @@ def dtype_code(dt: torch.dtype) -> int:
     raise _lib.DPError(f"unsupported dtype {dt}")
 
 
-# Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, shape, ev0, ev1).
+# Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, shape, dtype, ev0, ev1).
 _PROF: Optional[list] = None
 
 
@@ -40,16 +40,16 @@ def profile_begin() -> None:
 
 
 def profile_end() -> list:
-    """Stop recording; returns [(kind, flops, shape, milliseconds)] (synchronizes)."""
+    """Stop recording; returns [(kind, flops, shape, operand dtype, milliseconds)] (synchronizes)."""
     global _PROF
     rec, _PROF = _PROF or [], None
     torch.cuda.synchronize()
-    return [(k, f, sh, a.elapsed_time(b)) for (k, f, sh, a, b) in rec]
+    return [(k, f, sh, dt, a.elapsed_time(b)) for (k, f, sh, dt, a, b) in rec]
 
 
 class _Timed:
-    def __init__(self, kind: str, flops: float, shape: tuple = ()):
-        self.kind, self.flops, self.shape = kind, flops, shape
+    def __init__(self, kind: str, flops: float, shape: tuple = (), dtype=None):
+        self.kind, self.flops, self.shape, self.dtype = kind, flops, shape, dtype
 
     def __enter__(self):
         if _PROF is not None:
@@ -61,7 +61,7 @@ class _Timed:
     def __exit__(self, *exc):
         if _PROF is not None:
             self.e1.record()
-            _PROF.append((self.kind, self.flops, self.shape, self.e0, self.e1))
+            _PROF.append((self.kind, self.flops, self.shape, self.dtype, self.e0, self.e1))
         return False
 
 
@@ -85,6 +85,14 @@ class use_workspace:
         global _WS
         _WS = self.prev
         return False
+
+
+WS_ERROR_OFFSET = 4092   # dp_mi355x.h DP_GEMM_WS_ERROR_OFFSET: sticky stream-K timeout word
+
+
+def workspace_error(ws: torch.Tensor) -> int:
+    """The sticky stream-K error word of `ws` (synchronises)."""
+    return int(ws[WS_ERROR_OFFSET:WS_ERROR_OFFSET + 4].view(torch.int32).item())
 
 
 def gemm_workspace(device: torch.device) -> torch.Tensor:
@@ -181,7 +189,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
         return t.value, g.value
     _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None)
     kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
-    with _Timed(kind, 2.0 * M * N * K, (M, N, K)):
+    with _Timed(kind, 2.0 * M * N * K, (M, N, K), B.dtype):
         check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
 
 
@@ -214,14 +222,14 @@ def _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head, head_ps) -
 
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor, rows: int, cols: int,
               eps: float = 1e-6) -> None:
-    with _Timed("layernorm", 0.0, (rows, cols)):
+    with _Timed("layernorm", 0.0, (rows, cols), y.dtype):
         check(_lib.load().dp_layernorm(x.data_ptr(), cols, w.data_ptr(), b.data_ptr(), y.data_ptr(), cols,
                                        rows, cols, eps, dtype_code(y.dtype), _stream(y)), "dp_layernorm")
 
 
 def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int = 16,
               head_dim: int = 64) -> None:
-    with _Timed("attention", 4.0 * batch * heads * seq * seq * head_dim, (batch, seq)):
+    with _Timed("attention", 4.0 * batch * heads * seq * seq * head_dim, (batch, seq), out.dtype):
         check(_lib.load().dp_attention(qkv.data_ptr(), out.data_ptr(), batch, seq, heads, head_dim,
                                        head_dim ** -0.5, dtype_code(out.dtype), _stream(out)), "dp_attention")
 

@@ -87,7 +87,7 @@ def _model(device: torch.device, half_precision: bool):
     if key not in _MODEL:
         precision = torch.float16 if half_precision else torch.float32
         cfg = depth_pro.DEFAULT_MONODEPTH_CONFIG_DICT
-        if not os.path.exists(cfg.checkpoint_uri or "") and os.environ.get("DEPTH_PRO_SYNTHETIC", "1") == "1":
+        if not os.path.exists(cfg.checkpoint_uri or "") and os.environ.get("DEPTH_PRO_SYNTHETIC", "0") == "1":
             from depth_pro.depth_pro import DepthProConfig
 
             print(f"checkpoint {cfg.checkpoint_uri} not found: using synthetic weights (DEPTH_PRO_SYNTHETIC=1)")

@@ -3,7 +3,8 @@
 Run in the survey/build container only (it needs /root/reference, which does
 not exist on the GPU box):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py            # all fixtures
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --stages   # golden_stages_frame0.npz only
 
 What it does
 ------------
@@ -264,6 +265,58 @@ def sub(t: torch.Tensor, s: int) -> np.ndarray:
     return t[..., ::s, ::s].detach().float().numpy().copy()
 
 
+def stages(model, transform, t0):
+    """Per-stage intermediates of the reference forward on synthetic frame 0, for localising
+    a precision error stage by stage (tests/test_gpu_model.py::test_stage_parity).
+
+    Forward hooks on the reference modules (no reference code changed): the three ViT outputs
+    (final-norm tokens), the five encodings, the decoder's low-res projection, every fusion
+    block's output and the canonical inverse depth -- each sub-sampled to a small grid.
+    """
+    caps = {}
+
+    def keep(name):
+        def hook(mod, inp, out):
+            caps[name] = (out[0] if isinstance(out, tuple) else out).detach()
+        return hook
+
+    enc = model.encoder
+    hs = [enc.patch_encoder.register_forward_hook(keep("vit_patch")),
+          enc.image_encoder.register_forward_hook(keep("vit_image")),
+          model.fov.encoder[0].register_forward_hook(keep("vit_fov")),
+          model.decoder.convs[4].register_forward_hook(keep("lowres"))]
+    for i in range(5):
+        hs.append(model.decoder.fusions[i].register_forward_hook(keep(f"fusion{i}")))
+    enc_fwd = enc.forward
+
+    def enc_capture(x):
+        out = enc_fwd(x)
+        for i, o in enumerate(out):
+            caps[f"enc{i}"] = o.detach()
+        return out
+
+    enc.forward = enc_capture
+    with torch.no_grad():
+        canonical, fov_deg = model.forward(transform(frame(0)).unsqueeze(0))
+    enc.forward = enc_fwd
+    for h in hs:
+        h.remove()
+    out = {"frame_seed": 0, "fov_deg": fov_deg.numpy().reshape(-1)}
+    # ViT tokens [n, 577, 1024]: every 16th token of windows 0, 12, 34 (patch) / the image, every 4th channel
+    out["vit_patch"] = caps["vit_patch"][[0, 12, 34], ::16, ::4].numpy().copy()
+    out["vit_image"] = caps["vit_image"][0, ::16, ::4].numpy().copy()
+    out["vit_fov"] = caps["vit_fov"][0, ::16, ::4].numpy().copy()
+    # NCHW maps, sub-sampled to <= 24 x 24 spatially, every 4th channel
+    for k, t in caps.items():
+        if k.startswith("vit"):
+            continue
+        s = max(1, t.shape[-1] // 24)
+        out[k] = t[0, ::4, ::s, ::s].numpy().copy()
+    out["canonical_sub8"] = sub(canonical[0, 0], 8)
+    np.savez_compressed(os.path.join(HERE, "golden_stages_frame0.npz"), **out)
+    print(f"[golden] stages done ({time.time()-t0:.1f}s): " + ", ".join(f"{k}{list(np.shape(v))}" for k, v in out.items()))
+
+
 def main():
     t0 = time.time()
     torch.set_num_threads(len(os.sched_getaffinity(0)))
@@ -297,6 +350,8 @@ def main():
     sd = synthetic_state_dict(0)
     model.load_state_dict(sd, strict=True)
     print(f"[golden] synthetic weights loaded ({time.time()-t0:.1f}s)")
+    if "--stages" in sys.argv:
+        return stages(model, transform, t0)
     meta = {"keys": len(ref_sd), "params": int(sum(v.numel() for v in ref_sd.values())),
             "torch": torch.__version__}
 

@@ -6,7 +6,9 @@ import os
 import numpy as np
 import pytest
 
-import generate_depth_maps as G
+os.environ.setdefault("DEPTH_PRO_SYNTHETIC", "1")  # no checkpoint offline: synthetic weights
+
+import generate_depth_maps as G  # noqa: E402
 
 
 def test_colorize_matches_reference(golden_dir):

@@ -374,3 +374,29 @@ def test_head_pixel_shuffle_epilogue(cuda, dt):
     ref = F.conv_transpose2d(h0, wd, bd, stride=2)
     ref = F.relu(F.conv2d(F.relu(F.conv2d(ref, w2, b2, padding=1)), w4.reshape(1, 32, 1, 1), torch.tensor([0.25])))
     close(out, ref[0, 0], dt, "head HEAD_PS")
+
+
+def test_gemm_stream_k_timeout_sets_sticky_error_word(cuda):
+    """Fault injection (debug bit 64: every partial wait gives up at once): the sticky
+    error word of the workspace is set, survives the next launch's flag clear, and
+    Engine-level callers see it through ops.workspace_error."""
+    from depth_pro import _lib
+
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 20195, 3072, 1024           # 948 tiles on 256 workgroups: split tiles -> hand-offs
+    A = rnd(M, K, dt=torch.bfloat16, dev=cuda, gen=g)
+    B = rnd(N, K, dt=torch.bfloat16, dev=cuda, gen=g, scale=K ** -0.5)
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    ws = ops.gemm_workspace(cuda)
+    ops.gemm(A, B, C, M=M, N=N, K=K, tile=DP_TILE_STREAMK_256x256, workspace=ws)
+    assert ops.workspace_error(ws) == 0
+    lib = _lib.load()
+    lib.dp_gemm_debug_flags(64)
+    try:
+        ops.gemm(A, B, C, M=M, N=N, K=K, tile=DP_TILE_STREAMK_256x256, workspace=ws)
+        torch.cuda.synchronize()
+    finally:
+        lib.dp_gemm_debug_flags(0)
+    assert ops.workspace_error(ws) != 0
+    ops.gemm(A, B, C, M=M, N=N, K=K, tile=DP_TILE_STREAMK_256x256, workspace=ws)   # clean launch
+    assert ops.workspace_error(ws) != 0, "error word must be sticky across launches"

@@ -37,7 +37,7 @@ def main():
     eng.forward()
     rec = ops.profile_end()
     groups = {}
-    for kind, flops, shape, ms in rec:
+    for kind, flops, shape, _dt, ms in rec:
         g = groups.setdefault((kind, shape), [0, 0.0, 0.0])
         g[0] += 1
         g[1] += ms
