@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--dtype", choices=["bf16", "fp16", "mixed"], default="bf16",
+    ap.add_argument("--dtype", choices=["bf16", "fp16", "mixed"], default="mixed",
                     help="compute precision: bf16 / fp16 everywhere, or mixed = bf16 ViTs + f16 maps, "
                          "decoder and heads (depth_pro.depth_pro.PRECISION_MODES)")
     ap.add_argument("--no-graph", action="store_true")
@@ -299,7 +299,12 @@ def main():
             "config": {"workload": "BASELINE config 2/3: one 1536x1536 frame per GPU per step through "
                                    "DepthPro.infer (patch+image+FOV ViT-L, decoder, heads), hipGraph replay",
                        "global_batch": world, "frame": [1536, 1536], "parallelism": f"frame-dp{world}",
-                       "graph": not args.no_graph},
+                       "graph": not args.no_graph,
+                       "precision": {"bf16": "bf16 everywhere", "fp16": "f16 everywhere",
+                                     "mixed": "bf16 MFMA operands in the three ViT-L encoders, f16 in the "
+                                              "encoder maps / decoder / heads (fp32 accumulate, fp32 ViT "
+                                              "residual stream): the default, chosen to meet depth L1 < 1e-3"
+                                     }[args.dtype]},
             # dominant kernel: algorithmic FLOP per launch / its average HIP-event duration
             "roofline": {"bound": "mfma", "achieved": round(dom_tf, 1), "peak": PEAK_BF16_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(dom_tf / PEAK_BF16_TFLOPS, 4),

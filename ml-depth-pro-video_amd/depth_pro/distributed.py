@@ -1,11 +1,15 @@
 """Frame-parallel execution over one process per GPU (torch.distributed / RCCL).
 
 The video stream shards as independent frames: frame k runs on
-rank k mod N, with no collective on the data path.  Two collectives exist:
+rank k mod N, with no collective on the data path.  The collectives:
   * `broadcast_packed`: once at start-up rank 0 ships its packed (GEMM-ready,
     16-bit) weight set to every rank as ONE contiguous byte blob, so only rank 0
     reads/converts the checkpoint (one RCCL broadcast over xGMI);
-  * `gather_frames`: per step, the depth maps travel to rank 0 (RCCL gather).
+    (`create_model_and_transforms_shared` wraps it for the frame loops);
+  * `gather_frames`: per step, the depth maps travel to rank 0 (RCCL gather) --
+    bench.py's stream; the directory loop writes each rank's frames locally;
+  * the directory loop's resume list: rank 0 decides which frames still need work,
+    one `broadcast_object_list` before any rank writes.
 The same code runs over gloo on CPU tensors (tests/test_distributed.py).
 """
 
@@ -64,6 +68,30 @@ def broadcast_packed(packed: Optional[Dict[str, object]], device: torch.device, 
         else:
             out[m[0]] = m[2]
     return out
+
+
+def create_model_and_transforms_shared(config, device: torch.device, precision: torch.dtype = torch.float32,
+                                       src: int = 0):
+    """`create_model_and_transforms` for a process group: only rank `src` reads the checkpoint
+    and packs it (depth_pro.py:134-149 + engine.pack_weights); the packed 16-bit weight set
+    reaches every other rank as one RCCL broadcast (`broadcast_packed`), which builds its
+    engine on it directly (DepthPro.from_packed).  Every rank of the group must call this."""
+    from .depth_pro import DepthPro, Transform, create_model_and_transforms
+
+    rank = dist.get_rank()
+    info = [None]
+    packed = None
+    if rank == src:
+        model, transform = create_model_and_transforms(config, device=device, precision=precision)
+        packed = model.engine().P
+        info = [(model.use_fov_head, tuple(model.compute_dtype))]
+    dist.broadcast_object_list(info, src=src)
+    received = broadcast_packed(packed, device, src=src)
+    if rank == src:
+        del received           # rank src keeps the engine it packed
+        return model, transform
+    use_fov, codes = info[0]
+    return DepthPro.from_packed(received, device, codes, use_fov_head=use_fov), Transform(device, precision)
 
 
 def gather_frames(t: torch.Tensor, dst: int = 0, async_op: bool = False):

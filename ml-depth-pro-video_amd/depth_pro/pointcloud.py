@@ -28,7 +28,18 @@ def depth_to_3d(depth_in: torch.Tensor, focallength_px: Union[float, torch.Tenso
     focallength_px: a float, or the device scalar `infer` returns (read on the device);
     rgb: optional (height, width, 3) uint8 device tensor -> colours of the valid points.
     Returns (points (N, 3) fp64, valid_mask (height, width) bool, colors (N, 3) uint8 or None).
+    Reads the point count back (one synchronisation); `depth_to_points_async` does not.
     """
+    xyz, valid, cols, count = depth_to_points_async(depth_in, focallength_px, width, height, rgb)
+    n = int(count.item())
+    return xyz[:n], valid, (None if cols is None else cols[:n])
+
+
+def depth_to_points_async(depth_in: torch.Tensor, focallength_px: Union[float, torch.Tensor], width: int,
+                          height: int, rgb: Optional[torch.Tensor] = None):
+    """`depth_to_3d` without the read-back: (points buffer (H*W, 3) fp64, valid mask, colours buffer
+    or None, device int32 point count).  The first `count` rows of the buffers are the result;
+    nothing is synchronised, so a frame loop can queue it behind `infer` and read it later."""
     if depth_in.device.type != "cuda":
         raise _lib.DPError("depth_to_3d runs on the ROCm device (dp_depth_to_points)")
     d = depth_in.detach().to(torch.float32).contiguous()
@@ -52,9 +63,8 @@ def depth_to_3d(depth_in: torch.Tensor, focallength_px: Union[float, torch.Tenso
     check(_lib.load().dp_depth_to_points(d.data_ptr(), height, width, f_ptr, f_host, use_given,
                                          None if rgb is None else rgb.data_ptr(), rows.data_ptr(), xyz.data_ptr(),
                                          None if cols is None else cols.data_ptr(), stream), "dp_depth_to_points")
-    n = int(rows[height].item())
     valid = (d == d) & (d > 0)
-    return xyz[:n], valid, (None if cols is None else cols[:n])
+    return xyz, valid, cols, rows[height]
 
 
 def write_ply(path: str, points: np.ndarray, colors: Optional[np.ndarray] = None) -> str:

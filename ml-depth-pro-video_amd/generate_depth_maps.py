@@ -10,9 +10,11 @@ What changes is the loop: the model is created and packed ONCE
 (the reference rebuilds it for every frame, `:76-80`), the forward replays one
 HIP graph, frames are decoded by a thread pool ahead of the GPU, only the
 uint8 frame crosses PCIe (7 MB at 1536^2 instead of 28 MB fp32), and PNG
-encoding runs in writer threads behind the GPU.  Under `torchrun` the frame
-list is sharded k -> rank k mod N (one process per GPU); every rank writes its
-own frames.  cv2 is not required: PNGs are written with Pillow (pixel-identical
+encoding runs in writer threads behind the GPU.  Under `torchrun` (one process
+per GPU) only rank 0 reads and packs the checkpoint and RCCL-broadcasts the
+packed weights; the frame list is sharded k -> rank k mod N and every rank
+writes its own frames (`--resume`: rank 0 decides which frames are still
+missing, one broadcast before anything is written).  cv2 is not required: PNGs are written with Pillow (pixel-identical
 content; the reference's cv2 encoder may choose different zlib settings).
 """
 
@@ -26,10 +28,11 @@ import sys
 import threading
 import time
 from concurrent.futures import ThreadPoolExecutor
-from typing import Optional
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import depth_pro  # noqa: E402  (this package's drop-in)
@@ -81,20 +84,35 @@ def _resize_u8(image: np.ndarray, factor: float) -> np.ndarray:
 _MODEL = {}
 
 
+def _dist() -> Tuple[int, int]:
+    """(world, rank).  Under torchrun (WORLD_SIZE > 1) the process group is created here if the
+    caller has not: RCCL ("nccl") on the ROCm device, gloo otherwise."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 1, 0
+    if not dist.is_initialized():
+        if torch.cuda.is_available():
+            dev = _device()
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return dist.get_world_size(), dist.get_rank()
+
+
 def _model(device: torch.device, half_precision: bool):
-    """One model per (device, precision) per process (the reference reloads per frame)."""
+    """One model per (device, precision) per process (the reference reloads it per frame, :76-80).
+    In a process group only rank 0 reads and packs the checkpoint; the others receive the packed
+    weights over RCCL (distributed.create_model_and_transforms_shared)."""
     key = (str(device), bool(half_precision))
     if key not in _MODEL:
         precision = torch.float16 if half_precision else torch.float32
-        cfg = depth_pro.DEFAULT_MONODEPTH_CONFIG_DICT
-        if not os.path.exists(cfg.checkpoint_uri or "") and os.environ.get("DEPTH_PRO_SYNTHETIC", "0") == "1":
-            from depth_pro.depth_pro import DepthProConfig
-
-            print(f"checkpoint {cfg.checkpoint_uri} not found: using synthetic weights (DEPTH_PRO_SYNTHETIC=1)")
-            cfg = DepthProConfig(patch_encoder_preset="dinov2l16_384", image_encoder_preset="dinov2l16_384",
-                                 checkpoint_uri=None, decoder_features=256, use_fov_head=True,
-                                 fov_encoder_preset="dinov2l16_384")
-        model, transform = depth_pro.create_model_and_transforms(cfg, device=device, precision=precision)
+        cfg = depth_pro.depth_pro.run_config()       # DEPTH_PRO_SYNTHETIC=1: synthetic weights if no checkpoint
+        world, _ = _dist()
+        if world > 1:
+            model, transform = D.create_model_and_transforms_shared(cfg, device, precision)
+        else:
+            model, transform = depth_pro.create_model_and_transforms(cfg, device=device, precision=precision)
         model.eval()
         model.use_hip_graph(True)
         _MODEL[key] = (model, transform)
@@ -144,36 +162,50 @@ def generate_depth_map(image_path, output_path=None, downscale_factor=1.0, half_
         return None
 
 
-def _points(depth: torch.Tensor, f_px, image: np.ndarray, device: torch.device):
-    """Camera-space point cloud of one frame on the GPU (depth_to_3d, img_to_normalized_pointcloud.py:819-856)."""
-    h, w = depth.shape
-    rgb = torch.from_numpy(np.ascontiguousarray(image)).to(device, non_blocking=True)
-    pts, _, cols = PC.depth_to_3d(depth, f_px, w, h, rgb=rgb)
-    host_p = torch.empty(pts.shape, dtype=pts.dtype, pin_memory=True)
-    host_c = torch.empty(cols.shape, dtype=cols.dtype, pin_memory=True)
-    host_p.copy_(pts, non_blocking=True)
-    host_c.copy_(cols, non_blocking=True)
-    return host_p, host_c
+def output_name(image_path: str) -> str:
+    """`{base}_depth.png` (reference :187-188)."""
+    return f"{os.path.splitext(os.path.basename(image_path))[0]}_depth.png"
+
+
+def plan_frames(image_paths, output_dir: str, world: int, rank: int, resume: bool) -> List[int]:
+    """Indices of the frames this rank processes: the frames still to do (all of them, or with
+    `resume` those whose output file is missing -- decided by rank 0 alone and broadcast before
+    any rank writes, so every rank shards the same list), dealt round-robin over the ranks."""
+    todo = list(range(len(image_paths)))
+    if resume:
+        if rank == 0:
+            todo = [k for k in todo if not os.path.exists(os.path.join(output_dir, output_name(image_paths[k])))]
+        if world > 1:
+            box = [todo]
+            dist.broadcast_object_list(box, src=0)
+            todo = box[0]
+    return [todo[i] for i in D.shard_frames(len(todo), rank, world)]
 
 
 def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_factor=1.0, half_precision=False,
-                              colored=True, cmap="turbo", decode_workers=4, encode_workers=4, pointcloud=False):
+                              colored=True, cmap="turbo", decode_workers=4, encode_workers=4, pointcloud=False,
+                              resume=False, model=None):
     """Directory loop (reference :153-206), pipelined decode -> GPU -> encode, frame-sharded across ranks.
 
+    Every rank writes its own frames' files; each frame has exactly one owner.  resume=True skips
+    frames whose `{base}_depth.png` already exists (checkpoint/resume row).
     pointcloud=True also writes `{base}_points.ply` per frame: the reference's depth_to_3d
     back-projection with the frame's focal length (EXIF, or the FOV head's) and RGB colours
-    (the reference's ground-plane normalisation is out of scope)."""
+    (the reference's ground-plane normalisation is out of scope).
+    `model`: an already-built (model, transform) pair (tests); default: `_model`.
+    Returns the number of frames this rank wrote.
+    """
     os.makedirs(output_dir, exist_ok=True)
     image_paths = sorted(glob.glob(os.path.join(input_dir, pattern)))
     if not image_paths:
         print(f"No images found matching pattern {os.path.join(input_dir, pattern)}")
         return 0
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    mine = D.shard_frames(len(image_paths), rank, world)
+    world, rank = _dist()
+    mine = plan_frames(image_paths, output_dir, world, rank, resume)
     print(f"[rank {rank}/{world}] Found {len(image_paths)} images, processing {len(mine)}")
-    device = _device()
-    model, transform = _model(device, half_precision)
+    if model is None:
+        model = _model(_device(), half_precision)
+    model, transform = model
 
     successful = 0
     t0 = time.time()
@@ -183,7 +215,7 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
         pending = []
         for n, k in enumerate(mine):
             base_name = os.path.splitext(os.path.basename(image_paths[k]))[0]
-            output_path = os.path.join(output_dir, f"{base_name}_depth.png")
+            output_path = os.path.join(output_dir, output_name(image_paths[k]))
             try:
                 image, f_px = futs.pop(k).result()
                 if nxt < len(mine):
@@ -192,16 +224,23 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 with torch.no_grad():
                     pred = model.infer(transform(image), f_px=f_px)
                     depth = pred["depth"]
-                host = torch.empty(depth.shape, dtype=depth.dtype, pin_memory=True)
-                host.copy_(depth, non_blocking=True)
-                pc = _points(depth, pred["focallength_px"], image, device) if pointcloud else None
-                ev = torch.cuda.Event()
-                ev.record()
+                pc = None
+                if depth.is_cuda:
+                    # queue every device->host copy behind the frame; a writer thread waits on its event
+                    host = torch.empty(depth.shape, dtype=depth.dtype, pin_memory=True)
+                    host.copy_(depth, non_blocking=True)
+                    if pointcloud:
+                        pc = _points(depth, pred["focallength_px"], image)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                else:
+                    host, ev = depth, None
 
                 def _finish(host=host, ev=ev, path=output_path, pc=pc, base=base_name):
-                    ev.synchronize()
+                    if ev is not None:
+                        ev.synchronize()
                     if pc is not None:
-                        PC.write_ply(os.path.join(output_dir, f"{base}_points.ply"), pc[0].numpy(), pc[1].numpy())
+                        PC.write_ply(os.path.join(output_dir, f"{base}_points.ply"), *_points_host(pc))
                     return _encode(host.numpy(), path, colored, cmap)
 
                 pending.append(enc.submit(_finish))
@@ -210,12 +249,35 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 pending.append(None)
             print(f"[{n + 1}/{len(mine)}] Processing {base_name}")
         for f in pending:
-            if f is not None and f.result() is not None:
-                successful += 1
+            try:
+                if f is not None and f.result() is not None:
+                    successful += 1
+            except Exception as e:  # an encode / write failure skips that frame, like the reference
+                print(f"Error writing a depth map: {e}")
+    if hasattr(model, "engine"):
+        model.engine().check_status(block=True)
     dt = time.time() - t0
     print(f"Processing complete: {successful}/{len(mine)} images successfully processed "
           f"({len(mine) / max(dt, 1e-9):.2f} frames/s on rank {rank})")
     return successful
+
+
+def _points(depth: torch.Tensor, f_px, image: np.ndarray):
+    """Queue the frame's point cloud on the GPU (depth_to_3d, img_to_normalized_pointcloud.py:819-856)
+    without a host synchronisation: full-size buffers + the device point count."""
+    h, w = depth.shape
+    rgb = torch.from_numpy(np.ascontiguousarray(image)).to(depth.device, non_blocking=True)
+    xyz, _, cols, count = PC.depth_to_points_async(depth, f_px, w, h, rgb=rgb)
+    n_host = torch.empty((), dtype=torch.int32, pin_memory=True)
+    n_host.copy_(count, non_blocking=True)
+    return xyz, cols, n_host
+
+
+def _points_host(pc):
+    """Writer-thread side (after the frame's event): copy back exactly the valid points."""
+    xyz, cols, n_host = pc
+    n = int(n_host)
+    return xyz[:n].cpu().numpy(), cols[:n].cpu().numpy()
 
 
 def main():
@@ -229,13 +291,19 @@ def main():
     parser.add_argument("--raw", action="store_true", help="Save raw depth maps (grayscale) instead of colored ones")
     parser.add_argument("--pointcloud", action="store_true",
                         help="Also write {frame}_points.ply (depth_to_3d back-projection with RGB colours)")
+    parser.add_argument("--resume", action="store_true",
+                        help="Skip frames whose {frame}_depth.png already exists in --output_dir")
     parser.add_argument("--colormap", type=str, default="turbo",
                         choices=["turbo", "viridis", "plasma", "inferno", "magma", "cividis", "jet"],
                         help="Colormap for depth visualization")
     args = parser.parse_args()
     batch_generate_depth_maps(input_dir=args.input_dir, output_dir=args.output_dir, pattern=args.pattern,
                               downscale_factor=args.downscale_factor, half_precision=args.half_precision,
-                              colored=not args.raw, cmap=args.colormap, pointcloud=args.pointcloud)
+                              colored=not args.raw, cmap=args.colormap, pointcloud=args.pointcloud,
+                              resume=args.resume)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -5,6 +5,7 @@ not exist on the GPU box):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py            # all fixtures
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --stages   # golden_stages_frame0.npz only
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --io       # load_rgb + 4K infer fixtures
 
 What it does
 ------------
@@ -317,6 +318,83 @@ def stages(model, transform, t0):
     print(f"[golden] stages done ({time.time()-t0:.1f}s): " + ", ".join(f"{k}{list(np.shape(v))}" for k, v in out.items()))
 
 
+def io_images():
+    """Small synthetic images covering every branch of the reference load_rgb (utils.py:47-112):
+    EXIF orientations 1/3/6/8 and an ignored one (5), the three 35 mm focal-length tag names
+    (only the first is in PIL's EXIF table), a zero focal length, grey / palette / RGBA inputs."""
+    import io as _io
+
+    from PIL import Image
+
+    rng = np.random.default_rng(21)
+    out = {}
+
+    def jpeg(name, orient=None, f35=None, size=(48, 64)):
+        im = Image.fromarray(rng.integers(0, 256, size + (3,), dtype=np.uint8))
+        ex = Image.Exif()
+        if orient is not None:
+            ex[0x0112] = orient
+        if f35 is not None:
+            ex.get_ifd(0x8769)[0xA405] = f35
+        b = _io.BytesIO()
+        im.save(b, "JPEG", exif=ex, quality=95)
+        out[name] = b.getvalue()
+
+    def png(name, arr, mode=None):
+        b = _io.BytesIO()
+        Image.fromarray(arr, mode=mode).save(b, "PNG") if mode else Image.fromarray(arr).save(b, "PNG")
+        out[name] = b.getvalue()
+
+    jpeg("o1_f28.jpg", 1, 28)
+    jpeg("o3_f50.jpg", 3, 50, (40, 56))
+    jpeg("o6_f24.jpg", 6, 24)
+    jpeg("o8_nofocal.jpg", 8)
+    jpeg("o5_ignored.jpg", 5, 35)
+    jpeg("f0.jpg", None, 0)
+    png("grey.png", rng.integers(0, 256, (37, 53), dtype=np.uint8))
+    png("rgba.png", rng.integers(0, 256, (30, 40, 4), dtype=np.uint8))
+    pal = Image.fromarray(rng.integers(0, 256, (20, 24, 3), dtype=np.uint8)).convert("P", palette=Image.ADAPTIVE)
+    b = _io.BytesIO()
+    pal.save(b, "PNG")
+    out["palette.png"] = b.getvalue()
+    return out
+
+
+def io_fixtures(ref, model, transform, t0):
+    """Fixtures for the host-side input path and config 5:
+
+    * golden_load_rgb.npz -- the reference load_rgb on io_images() (file bytes + its outputs);
+    * golden_infer_4k.npz -- the reference infer on a synthetic 3840x2160 frame (config 5's
+      resize path: 4K -> 1536^2 -> depth resized back), f_px from the FOV head.
+    """
+    import tempfile
+
+    imgs = io_images()
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        for i, (name, data) in enumerate(sorted(imgs.items())):
+            path = os.path.join(d, name)
+            with open(path, "wb") as f:
+                f.write(data)
+            img, icc, fpx = ref.load_rgb(path)
+            out[f"file{i}_name"] = np.array(name)
+            out[f"file{i}_bytes"] = np.frombuffer(data, dtype=np.uint8).copy()
+            out[f"file{i}_img"] = img
+            out[f"file{i}_fpx"] = np.array(np.nan if fpx is None else float(fpx))
+            out[f"file{i}_icc"] = np.array(icc is not None)
+    out["n_files"] = np.array(len(imgs))
+    np.savez_compressed(os.path.join(HERE, "golden_load_rgb.npz"), **out)
+    print(f"[golden] load_rgb fixtures: {len(imgs)} files ({time.time()-t0:.1f}s)")
+
+    img4k = frame(5, 2160, 3840)
+    with torch.no_grad():
+        p = model.infer(transform(img4k), f_px=None)
+    np.savez_compressed(os.path.join(HERE, "golden_infer_4k.npz"), frame_seed=5, H=2160, W=3840,
+                        depth_sub16=sub(p["depth"], 16), depth_stats=stats(p["depth"]),
+                        f_px=np.array(float(p["focallength_px"])))
+    print(f"[golden] infer 4K done ({time.time()-t0:.1f}s): f_px={float(p['focallength_px']):.3f}")
+
+
 def main():
     t0 = time.time()
     torch.set_num_threads(len(os.sched_getaffinity(0)))
@@ -352,6 +430,8 @@ def main():
     print(f"[golden] synthetic weights loaded ({time.time()-t0:.1f}s)")
     if "--stages" in sys.argv:
         return stages(model, transform, t0)
+    if "--io" in sys.argv:
+        return io_fixtures(ref, model, transform, t0)
     meta = {"keys": len(ref_sd), "params": int(sum(v.numel() for v in ref_sd.values())),
             "torch": torch.__version__}
 

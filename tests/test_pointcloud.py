@@ -3,7 +3,9 @@
 The reference function (img_to_normalized_pointcloud.py:819-856) lives in a module that
 imports open3d / cv2 at the top, so the oracle restates it (oracle.depth_pro_oracle.depth_to_3d,
 same numpy expression); the GPU result must equal it bit for bit (fp64, same op order,
-same row-major point order).  The PLY writer is checked by a round trip.
+same row-major point order).  Both are pinned to the reference function itself:
+tests/golden/golden_pointcloud.npz holds its outputs (lifted out of the reference module
+with `ast` by make_golden_frameloop.py).  The PLY writer is checked by a round trip.
 """
 
 import numpy as np
@@ -30,6 +32,29 @@ def test_oracle_depth_to_3d_known_values():
     assert valid.tolist() == [[True, False], [False, True]]
     # (u, v) = (0, 0): x = -(0 - 1) * 1 / 2 = 0.5, y = 0.5; (1, 1): x = -(1 - 1) * 4 / 2 = 0
     np.testing.assert_array_equal(pts, [[0.5, 0.5, 1.0], [0.0, 0.0, 4.0]])
+
+
+def _golden_cases(golden_dir):
+    g = np.load(f"{golden_dir}/golden_pointcloud.npz")
+    for i in range(int(g["n_cases"])):
+        yield g[f"case{i}_depth"], float(g[f"case{i}_f"]), g[f"case{i}_points"], g[f"case{i}_valid"]
+
+
+def test_oracle_depth_to_3d_matches_reference_function(golden_dir):
+    for d, f, pts_ref, valid_ref in _golden_cases(golden_dir):
+        h, w = d.shape
+        pts, valid = O.depth_to_3d(d, f, w, h)
+        assert np.array_equal(valid, valid_ref)
+        assert pts.dtype == pts_ref.dtype and np.array_equal(pts, pts_ref)
+
+
+@pytest.mark.gpu
+def test_depth_to_points_matches_reference_function(cuda, golden_dir):
+    for d, f, pts_ref, valid_ref in _golden_cases(golden_dir):
+        h, w = d.shape
+        pts, vmask, _ = PC.depth_to_3d(torch.from_numpy(d).to(cuda), f, w, h)
+        assert np.array_equal(vmask.cpu().numpy(), valid_ref)
+        assert np.array_equal(pts.cpu().numpy(), pts_ref)        # bit-exact fp64
 
 
 def test_ply_round_trip(tmp_path):
