@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 3
+#define DP_ABI_VERSION 4
 int dp_abi_version(void);
 
 /*
@@ -203,6 +203,16 @@ int dp_vit_cls_rows(float* x, const float* cls, const float* pos, int32_t n_imag
  */
 int dp_merge_windows(const void* src, int32_t src_dtype, int64_t ld_src, int32_t first_window,
                      int32_t steps, int32_t padding, void* dst, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_merge_windows_range: dp_merge_windows restricted to the windows w_lo <= w < w_hi of the
+ * steps x steps grid (w = row * steps + column); the other pixels of dst are not written.
+ * For a patch encoder run as several independent window groups (each merges its own share
+ * of a hooked block's output before it moves on).
+ */
+int dp_merge_windows_range(const void* src, int32_t src_dtype, int64_t ld_src, int32_t first_window,
+                           int32_t steps, int32_t padding, int32_t w_lo, int32_t w_hi, void* dst,
+                           int32_t dtype, dp_stream_t stream);
 
 /*
  * dp_fov_tail: final FOV conv 6x6 (32 -> 1) + bias on the 6x6x32 NHWC map

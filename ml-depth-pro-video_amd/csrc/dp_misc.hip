@@ -238,9 +238,12 @@ __device__ __forceinline__ void merge_axis(int Y, int steps, int pad, int& j, in
   yy = pad + (y2 - (j - 1) * mid);
 }
 
+// Pixels whose source window (j * steps + ii) lies outside [wlo, whi) are left untouched:
+// a caller that runs the windows in several independent row groups merges each group's
+// share as soon as that group reaches the hooked block.
 template <typename K_, int SRC>
 __global__ void merge_kernel(const void* __restrict__ src, long long ld, int w0, int steps, int pad, int S,
-                             u16* __restrict__ dst) {
+                             u16* __restrict__ dst, int wlo, int whi) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (pixel, 8-channel group)
   if (i >= (long long)S * S * 128) return;
   const int g = i % 128;
@@ -249,7 +252,9 @@ __global__ void merge_kernel(const void* __restrict__ src, long long ld, int w0,
   int j, yy, ii, xx;
   merge_axis(Y, steps, pad, j, yy);
   merge_axis(X, steps, pad, ii, xx);
-  const long long row = (long long)(w0 + j * steps + ii) * 577 + 1 + yy * 24 + xx;
+  const int win = j * steps + ii;
+  if (win < wlo || win >= whi) return;
+  const long long row = (long long)(w0 + win) * 577 + 1 + yy * 24 + xx;
   uint32_t pk[4];
   if constexpr (SRC == DP_F32) {
     const float* s = (const float*)src + row * ld + g * 8;
@@ -385,19 +390,26 @@ extern "C" int dp_vit_cls_rows(float* x, const float* cls, const float* pos, int
 
 extern "C" int dp_merge_windows(const void* src, int32_t src_dtype, int64_t ld, int32_t w0, int32_t steps,
                                 int32_t pad, void* dst, int32_t dtype, dp_stream_t stream) {
+  return dp_merge_windows_range(src, src_dtype, ld, w0, steps, pad, 0, steps * steps, dst, dtype, stream);
+}
+
+extern "C" int dp_merge_windows_range(const void* src, int32_t src_dtype, int64_t ld, int32_t w0, int32_t steps,
+                                      int32_t pad, int32_t wlo, int32_t whi, void* dst, int32_t dtype,
+                                      dp_stream_t stream) {
   if (!src || !dst) return DP_ERR_ARG;
   if (steps <= 0 || pad < 0 || (steps > 1 && 24 - 2 * pad <= 0) || ld % 8) return DP_ERR_SHAPE;
+  if (wlo < 0 || whi > steps * steps || wlo >= whi) return DP_ERR_SHAPE;
   const int S = steps == 1 ? 24 : 2 * (24 - pad) + (steps - 2) * (24 - 2 * pad);
   const long long total = (long long)S * S * 128;
   hipStream_t s = (hipStream_t)stream;
   dim3 g(blocks_for(total, 256));
   if (src_dtype != DP_F32 && src_dtype != dtype) return DP_ERR_DTYPE;
   if (dtype == DP_BF16) {
-    if (src_dtype == DP_F32) hipLaunchKernelGGL((merge_kernel<KBF16, DP_F32>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
-    else hipLaunchKernelGGL((merge_kernel<KBF16, DP_BF16>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
+    if (src_dtype == DP_F32) hipLaunchKernelGGL((merge_kernel<KBF16, DP_F32>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst, wlo, whi);
+    else hipLaunchKernelGGL((merge_kernel<KBF16, DP_BF16>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst, wlo, whi);
   } else if (dtype == DP_F16) {
-    if (src_dtype == DP_F32) hipLaunchKernelGGL((merge_kernel<KF16, DP_F32>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
-    else hipLaunchKernelGGL((merge_kernel<KF16, DP_F16>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst);
+    if (src_dtype == DP_F32) hipLaunchKernelGGL((merge_kernel<KF16, DP_F32>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst, wlo, whi);
+    else hipLaunchKernelGGL((merge_kernel<KF16, DP_F16>), g, dim3(256), 0, s, src, ld, w0, steps, pad, S, (u16*)dst, wlo, whi);
   } else {
     return DP_ERR_DTYPE;
   }

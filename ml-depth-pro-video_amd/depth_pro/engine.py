@@ -201,6 +201,22 @@ class _ViTBuffers:
         self.out = self.h if out_dt == dt else self.a.view(out_dt)
 
 
+class _Rows:
+    """Rows [r0, r1) of a _ViTBuffers as contiguous views (one window group of the patch encoder)."""
+
+    def __init__(self, buf: _ViTBuffers, r0: int, r1: int):
+        self.rows = r1 - r0
+        for n in ("x", "h", "qkv", "a", "m", "out"):
+            setattr(self, n, getattr(buf, n)[r0:r1])
+
+
+def window_groups(n: int):
+    """Split the 35 windows into n contiguous groups of near-equal size: [(w0, w1), ...]."""
+    n = max(1, min(int(n), NWIN))
+    cuts = [round(i * NWIN / n) for i in range(n + 1)]
+    return [(cuts[i], cuts[i + 1]) for i in range(n)]
+
+
 class Engine:
     """One frame (batch 1) per forward; static workspace (~4 GB)."""
 
@@ -269,14 +285,19 @@ class Engine:
         # stream-K GEMM scratch, one per stream that issues GEMMs (main / side)
         self.ws_main = ops.gemm_workspace(dev)
         self.ws_side = ops.gemm_workspace(dev)
+        # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
+        # `DP_PATCH_GROUPS` window groups on their own streams, so one group's bandwidth-bound
+        # phases (LayerNorm, GEMM epilogues) overlap another group's MFMA phases.
+        self.set_patch_groups(int(os.environ.get("DP_PATCH_GROUPS", "1")), _init=True)
         # their sticky error words (dp_mi355x.h DP_GEMM_WS_ERROR_OFFSET), read back asynchronously
         # after every forward into pinned memory and checked by `check_status`
-        self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32)
-                         for w in (self.ws_main, self.ws_side)]
-        self._err_host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        wss = [self.ws_main, self.ws_side] + self.ws_groups
+        self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32) for w in wss]
+        self._err_host = torch.zeros(len(wss), dtype=torch.int32, pin_memory=True)
         self._err_ev: Optional[torch.cuda.Event] = None
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
         self.serial_side = False   # True: run the side encoders on the current stream (profiling)
+
         # FOV encoder + head beside the decoder instead of the patch encoder (measured: 0.3 ms
         # slower on MI355X, so off by default; DP_FOV_LATE=1 to try)
         self.fov_late = os.environ.get("DP_FOV_LATE", "0") == "1"
@@ -347,6 +368,39 @@ class Engine:
         ops.gemm(d["y"], P[p + "out.w"], self.feats, M=s * s, N=256, K=256, bias=P[p + "out.b"])
         return self.feats
 
+    def set_patch_groups(self, n: int, _init: bool = False) -> None:
+        """Run the patch encoder as `n` concurrent window groups (drops a captured graph)."""
+        self.patch_groups = window_groups(n)
+        self.gstreams = [torch.cuda.Stream(device=self.dev) for _ in self.patch_groups[1:]]
+        self.ws_groups = [ops.gemm_workspace(self.dev) for _ in self.patch_groups[1:]]
+        if not _init:
+            self.graph = None
+            wss = [self.ws_main, self.ws_side] + self.ws_groups
+            self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32) for w in wss]
+            self._err_host = torch.zeros(len(wss), dtype=torch.int32, pin_memory=True)
+            self._err_ev = None
+
+    def _patch_groups(self, main) -> None:
+        """The patch encoder as independent window groups, group g on stream g (group 0 on
+        `main`); each merges its own windows' share of the hooked block outputs."""
+        vp = self.vp
+        for g, (w0, w1) in enumerate(self.patch_groups):
+            serial = self.serial_side or g == 0
+            st = main if serial else self.gstreams[g - 1]
+            ws = self.ws_main if serial else self.ws_groups[g - 1]
+            if st is not main:
+                st.wait_stream(main)
+            lo, hi = min(w0, 25), min(w1, 25)   # their windows in the 5 x 5 hook grid
+            hooks = {}
+            if lo < hi:
+                hooks = {5: lambda lo=lo, hi=hi: ops.merge_windows(vp.x, 0, 5, 3, self.lat0, windows=(lo, hi)),
+                         11: lambda lo=lo, hi=hi: ops.merge_windows(vp.x, 0, 5, 3, self.lat1, windows=(lo, hi))}
+            with torch.cuda.stream(st), ops.use_workspace(ws):
+                self._vit("encoder.patch_encoder.", _Rows(vp, w0 * TOK, w1 * TOK), w1 - w0, w0 * PTOK, hooks)
+        if not self.serial_side:
+            for st in self.gstreams:
+                main.wait_stream(st)
+
     # -------------------------------------------------------------- forward
     def _image_encoder(self):
         """Image encoder (+ lowres upsample): ~2.5 % of the frame's FLOPs at M = 577
@@ -404,11 +458,14 @@ class Engine:
                     if self.use_fov and not self.fov_late:
                         self._fov_encoder()
         vp = self.vp
-        hooks = {
-            5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
-            11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
-        }
-        self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks)
+        if len(self.patch_groups) == 1:
+            hooks = {
+                5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
+                11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
+            }
+            self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks)
+        else:
+            self._patch_groups(main)
         ops.merge_windows(vp.out, 0, 5, 3, self.f0)
         ops.merge_windows(vp.out, 25, 3, 6, self.f1)
         ops.merge_windows(vp.out, 34, 1, 0, self.f2)

@@ -259,9 +259,16 @@ def vit_cls_rows(x: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor, n: int) 
 
 
 def merge_windows(src: torch.Tensor, first_window: int, steps: int, padding: int, dst: torch.Tensor,
-                  ld: int = 1024) -> None:
-    check(_lib.load().dp_merge_windows(src.data_ptr(), dtype_code(src.dtype), ld, first_window, steps, padding,
-                                       dst.data_ptr(), dtype_code(dst.dtype), _stream(dst)), "dp_merge_windows")
+                  ld: int = 1024, windows: Optional[tuple] = None) -> None:
+    """windows=(lo, hi): only grid windows lo <= w < hi (dp_merge_windows_range)."""
+    lib = _lib.load()
+    if windows is None:
+        check(lib.dp_merge_windows(src.data_ptr(), dtype_code(src.dtype), ld, first_window, steps, padding,
+                                   dst.data_ptr(), dtype_code(dst.dtype), _stream(dst)), "dp_merge_windows")
+    else:
+        check(lib.dp_merge_windows_range(src.data_ptr(), dtype_code(src.dtype), ld, first_window, steps, padding,
+                                         int(windows[0]), int(windows[1]), dst.data_ptr(), dtype_code(dst.dtype),
+                                         _stream(dst)), "dp_merge_windows_range")
 
 
 def fov_tail(x6: torch.Tensor, w: torch.Tensor, bias: float, out: torch.Tensor) -> None:

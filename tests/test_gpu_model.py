@@ -210,3 +210,24 @@ def test_config5_4k_frame_vs_reference(model, golden_dir):
     e_f = abs(float(p["focallength_px"]) - float(g["f_px"])) / float(g["f_px"])
     print(f"\n[{m.tag}] 4K depth rel-L1 {e_d:.3e}  f_px {float(p['focallength_px']):.3f} vs {float(g['f_px']):.3f}")
     assert e_d < m.tol["depth"] and e_f < m.tol["fpx"]
+
+
+@pytest.mark.parametrize("groups", [2, 3])
+def test_patch_window_groups_match_single_group(model, groups):
+    """The patch encoder run as concurrent window groups (Engine.set_patch_groups) gives the same
+    canonical inverse depth and FOV as one group: the same per-element K order everywhere."""
+    m, transform = model
+    e = m.engine()
+    x = transform(frame(6))
+    n0 = len(e.patch_groups)
+    try:
+        e.set_patch_groups(1)
+        c1, f1 = (t.clone() for t in m.forward(x.unsqueeze(0)))
+        e.set_patch_groups(groups)
+        cg, fg = m.forward(x.unsqueeze(0))
+        torch.cuda.synchronize()
+        d = (cg - c1).abs().max().item()
+        print(f"\n[{m.tag}] {groups} window groups: max|d canonical| {d:.3e}")
+        assert torch.equal(cg, c1) and torch.equal(fg, f1)
+    finally:
+        e.set_patch_groups(n0)

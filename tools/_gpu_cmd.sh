@@ -1,1 +1,1 @@
-bash tools/gpu_check.sh r02d tests smoke bench prof
+bash tools/gpu_check.sh r02f sq pmc

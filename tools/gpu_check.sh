@@ -2,7 +2,7 @@
 # One bounded GPU session (run on the gpurun box from the repo root):
 #   GPU tests -> bench line -> rocprofv3 kernel-trace stats -> FETCH/WRITE PMC passes.
 # Every GPU step has its own time limit; the first failure ends the script.
-# Usage: tools/gpu_check.sh <tag> [tests|bench|prof|pmc ...]   (default: all four)
+# Usage: tools/gpu_check.sh <tag> [tests|smoke|bench|prof|pmc|sq ...]   (default: tests bench prof pmc)
 set -eo pipefail
 TAG=${1:-r01}
 shift || true
@@ -29,6 +29,14 @@ for S in $STEPS; do
         -- python3 tools/frame_once.py > $OUT/pmc_fetch.log 2>&1
       timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc \
         -- python3 tools/frame_once.py > $OUT/pmc_write.log 2>&1 ;;
+    sq)
+      # SQ wave-state / MFMA-busy passes over an eager forward (tools/pmc_sq.py), one pass each
+      timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --output-format csv \
+        -d $OUT/pmc_sq1 -o pmc -- python3 tools/frame_once.py > $OUT/pmc_sq1.log 2>&1
+      timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
+        SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv \
+        -d $OUT/pmc_sq2 -o pmc -- python3 tools/frame_once.py > $OUT/pmc_sq2.log 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
   echo "step $S ok"
