@@ -16,7 +16,9 @@
 // registers; 4 workgroups (16 waves) per CU.
 // Softmax: scale folded into one FMA per score, exp2, a deferred running-max
 // rescale, and row sums taken by the matrix core (an all-ones V^T block).
-// The last, partial key tile is masked and skips its empty 32-key half.
+// A last, partial key tile is masked and skips its empty 32-key half; one or two
+// leftover keys (the ViT's 577 = 9 x 64 + 1) go through the VALU instead (tail_key).
+#include <cstdlib>
 #include <type_traits>
 
 #include "dp_common.h"
@@ -29,6 +31,7 @@ constexpr int HD = 64;       // head dim
 constexpr int KS = 72;       // output staging row stride (elements): conflict-free b128 reads
 constexpr int VRB = 128;     // K / V tile row bytes (64 d x 16 bit), swizzled
 constexpr int TILE_B = KT * VRB;   // 8 KiB per operand tile
+constexpr int TAIL_VALU = 2;       // leftover keys handled on the VALU instead of a partial tile
 
 typedef short v4s_t __attribute__((ext_vector_type(4)));
 
@@ -53,7 +56,9 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
       : "memory");
 }
 
-template <typename K_>
+// VSUM: row sums of P as f32 VALU adds (2 packed adds per 4 scores) instead of an MFMA
+// against an all-ones operand (4 of the 20 MFMAs of a tile).
+template <typename K_, bool VSUM>
 __global__ void __launch_bounds__(256, 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
   __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
@@ -118,6 +123,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   };
 
   f32x16_t o[2], osum;   // osum: row sums of P, from an all-ones A operand (every row equal)
+  f32x2_t lsum = {0.f, 0.f};   // VSUM: this lane's share of its query's row sum
   #pragma unroll
   for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; osum[i] = 0.f; }
   const uint32_t one2 = K_::pack2(1.f, 1.f);
@@ -178,6 +184,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_upd);
       #pragma unroll
       for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; osum[i] *= alpha; }
+      lsum *= alpha;
       m_run = m_upd;
     }
     uint4 pf[2][2];
@@ -191,6 +198,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
           const float p0 = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * st + 2 * jj], sl2, -m_run));
           const float p1 = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * st + 2 * jj + 1], sl2, -m_run));
           w[jj] = K_::pack2(p0, p1);
+          if constexpr (VSUM) lsum += f32x2_t{p0, p1};
         }
         pf[kb][st] = make_uint4(w[0], w[1], w[2], w[3]);
       }
@@ -210,29 +218,88 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
           const uint2 a = __builtin_bit_cast(uint2, lo), c = __builtin_bit_cast(uint2, up);
           o[db] = K_::mfma32(make_uint4(a.x, a.y, c.x, c.y), pf[kb][st], o[db]);
         }
-        osum = K_::mfma32(ones, pf[kb][st], osum);
+        if constexpr (!VSUM) osum = K_::mfma32(ones, pf[kb][st], osum);
       }
     }
+  };
+
+  // One leftover key (seq = 64 n + r, r <= TAIL_VALU: the ViT's 577 = 9 x 64 + 1) costs a
+  // whole masked MFMA tile on the partial path; on the VALU it is a 64-d dot product per
+  // query (each lane holds half of its query's dims: FMAs + one permlane32 swap), the same
+  // online-softmax update, and a rank-1 update of O (p rounded to 16 bits like the MFMA path's P).
+  auto tail_key = [&](int key) {
+    const u16* kr = base + (long long)key * ldq + kcol;
+    const u16* vr = base + (long long)key * ldq + vcol;
+    float dot = 0.f;
+    #pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const uint4 kv = *(const uint4*)(kr + 16 * ks + 8 * hi);
+      const uint32_t kw[4] = {kv.x, kv.y, kv.z, kv.w};
+      const uint32_t qw[4] = {qf[ks].x, qf[ks].y, qf[ks].z, qf[ks].w};
+      #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dot = fmaf(K_::to_f(qw[j] & 0xffff), K_::to_f(kw[j] & 0xffff), dot);
+        dot = fmaf(K_::to_f(qw[j] >> 16), K_::to_f(kw[j] >> 16), dot);
+      }
+    }
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dot), __float_as_uint(dot), false, false);
+      dot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    }
+    const float sc = dot * sl2;
+    if (__builtin_amdgcn_ballot_w64(sc > m_run + 8.f)) {
+      const float m_upd = fmaxf(m_run, sc);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_upd);
+      #pragma unroll
+      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; osum[i] *= alpha; }
+      lsum *= alpha;
+      m_run = m_upd;
+    }
+    const float pr = __builtin_amdgcn_exp2f(sc - m_run);
+    const float p = K_::to_f(K_::from_f(pr));
+    osum[0] += p;
+    if constexpr (VSUM) lsum[0] += 0.5f * p;   // both half-waves add it: the swap below doubles it
+    #pragma unroll
+    for (int db = 0; db < 2; ++db)
+      #pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint2 vv = *(const uint2*)(vr + db * 32 + 8 * g + 4 * hi);
+        o[db][4 * g + 0] = fmaf(p, K_::to_f(vv.x & 0xffff), o[db][4 * g + 0]);
+        o[db][4 * g + 1] = fmaf(p, K_::to_f(vv.x >> 16), o[db][4 * g + 1]);
+        o[db][4 * g + 2] = fmaf(p, K_::to_f(vv.y & 0xffff), o[db][4 * g + 2]);
+        o[db][4 * g + 3] = fmaf(p, K_::to_f(vv.y >> 16), o[db][4 * g + 3]);
+      }
   };
 
   // tile t lives in stage t & 1.  Top of step t: tile t's DMA was issued one step
   // earlier (own pieces: vmcnt(0); everyone's: the barrier, which also certifies
   // that every wave finished tile t-1, whose stage now receives tile t+1).
-  const int ntiles = (seq + KT - 1) / KT, nfull = seq / KT;
-  issue(0, 0);
+  const int ntiles = (seq + KT - 1) / KT, nfull = seq / KT, rem = seq - nfull * KT;
+  const bool valu_tail = rem > 0 && rem <= TAIL_VALU;
+  const int nmma = valu_tail ? nfull : ntiles;     // tiles that go through the MFMAs
+  if (nmma > 0) issue(0, 0);
   for (int t = 0; t < nfull; ++t) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (t + 1 < ntiles) issue((t + 1) * KT, (t + 1) & 1);
+    if (t + 1 < nmma) issue((t + 1) * KT, (t + 1) & 1);
     do_tile(t, std::false_type{});
   }
-  if (nfull < ntiles) {
+  if (nfull < nmma) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     do_tile(nfull, std::true_type{});
+  }
+  if (valu_tail && active) {
+    for (int kk = 0; kk < rem; ++kk) tail_key(nfull * KT + kk);
   }
   __syncthreads();
   // ---- normalise and store: stage the wave's 32 x 64 output through LDS so each
   // query row leaves as whole 128-B lines
-  const float inv = 1.f / osum[0];
+  float rowsum = osum[0];
+  if constexpr (VSUM) {
+    const float l = lsum[0] + lsum[1];
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+    rowsum = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const float inv = 1.f / rowsum;
   u16* stg = (u16*)&smem[0][0] + wave * 32 * KS;   // 32 rows x KS (padded) per wave (18 KiB of 32)
   #pragma unroll
   for (int db = 0; db < 2; ++db)
@@ -265,12 +332,12 @@ extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t s
   dim3 grid(nq * heads * batch);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == DP_BF16)
-    hipLaunchKernelGGL(attn_kernel<KBF16>, grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-  else if (dtype == DP_F16)
-    hipLaunchKernelGGL(attn_kernel<KF16>, grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-  else
-    return DP_ERR_DTYPE;
+  static const bool vsum = [] { const char* e = getenv("DP_ATTN_VSUM"); return e && e[0] == '1'; }();
+  if (dtype != DP_BF16 && dtype != DP_F16) return DP_ERR_DTYPE;
+#define DP_ATTN(K, V) hipLaunchKernelGGL((attn_kernel<K, V>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2)
+  if (dtype == DP_BF16) { if (vsum) DP_ATTN(KBF16, true); else DP_ATTN(KBF16, false); }
+  else { if (vsum) DP_ATTN(KF16, true); else DP_ATTN(KF16, false); }
+#undef DP_ATTN
   DP_CHECK_LAUNCH();
   return 0;
 }

@@ -112,9 +112,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int
     lib.dp_gemm_workspace_size.restype = ctypes.c_int64
+    lib.dp_gemm_debug_flags.argtypes = [ctypes.c_int]
+    lib.dp_gemm_debug_flags.restype = ctypes.c_int
     ver = lib.dp_abi_version()
     if ver != DP_ABI_VERSION:
         raise DPError(f"{path} has ABI version {ver}, expected {DP_ABI_VERSION}; rebuild it")
+    dbg = int(os.environ.get("DP_GEMM_DEBUG", "0") or 0)   # ablation / A-B switches (tools, bench)
+    if dbg:
+        lib.dp_gemm_debug_flags(dbg)
     _lib = lib
     return lib
 

@@ -140,11 +140,19 @@ def test_head_conv_with_fused_1x1(cuda, dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("batch,seq", [(2, 577), (1, 100), (3, 64), (1, 1)])
-def test_attention(cuda, dt, batch, seq):
+@pytest.mark.parametrize("batch,seq,spike", [(2, 577, False), (1, 100, False), (3, 64, False), (1, 1, False),
+                                             (2, 66, False), (1, 2, False), (1, 67, False),
+                                             (2, 577, True), (1, 130, True)])
+def test_attention(cuda, dt, batch, seq, spike):
+    """seq 577 / 66 / 2 / 130 end in 1-2 leftover keys (the VALU tail), 100 / 67 in a partial
+    MFMA tile.  spike: the LAST key of every sequence is the scaled query of token 0, so that
+    query's running max jumps inside the tail -- the rescale branch there is exercised."""
     g = torch.Generator().manual_seed(seq)
     H, hd = 16, 64
     qkv = rnd(batch * seq, 3 * H * hd, dt=dt, dev=cuda, gen=g, scale=2.0)
+    if spike:
+        x = qkv.view(batch, seq, 3, H, hd)
+        x[:, seq - 1, 1] = (x[:, 0, 0].float() * 4.0).to(dt)
     out = torch.empty(batch * seq, H * hd, dtype=dt, device=cuda)
     ops.attention(qkv, out, batch, seq, H, hd)
     q, k, v = qkv.float().reshape(batch, seq, 3, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
