@@ -129,14 +129,16 @@ int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 
 /*
  * Bytes of workspace the stream-K engine needs (flags + one fp32 256x256 partial
- * tile per persistent workgroup).  The caller zeroes it once after allocation; its
- * hand-off flags are cleared by dp_gemm itself (a memset node on the same stream)
- * before each stream-K launch, the rest is scratch -- except the ERROR WORD: the
+ * tile per persistent workgroup).  The caller zeroes it once after allocation; every
+ * hand-off flag a stream-K launch sets is reset by the workgroup that consumes it, so
+ * the flags are zero again whenever a launch ends (no per-launch clearing, nothing but
+ * kernels touches it -- graph-replay safe), the rest is scratch -- except the ERROR WORD: the
  * uint32 at byte offset DP_GEMM_WS_ERROR_OFFSET becomes non-zero when a stream-K
  * launch on this workspace gave up waiting for another workgroup's partial tile
  * (bounded spin; the output of that launch is then wrong).  It is sticky: nothing
  * but the caller clears it, so one read after a whole forward / graph replay covers
- * every launch in it.
+ * every launch in it.  After a timeout the flags may be left set: zero the first 1 KiB
+ * (or the whole workspace) before reusing it.
  */
 #define DP_GEMM_WS_ERROR_OFFSET 4092
 int64_t dp_gemm_workspace_size(void);

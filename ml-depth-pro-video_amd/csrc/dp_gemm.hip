@@ -1061,8 +1061,7 @@ constexpr int SK_STAGE = 2 * SK_A_BYTES;         // A + B
 constexpr int SK_RING = 2 * SK_STAGE;            // 2 stages: 128 KiB
 constexpr int SK_EPI = 8 * 16 * 64 * 4;          // 8 waves x 16 rows x 64 fp32
 constexpr int SK_TILE_F = 256 * 256;             // floats per partial slot
-constexpr long long SK_FLAG_BYTES = 4096;        // flags [0, G) (cleared per launch), error word at [1023] (sticky)
-constexpr long long SK_CLEAR_BYTES = 4 * 256;     // the per-launch memset: flags only
+constexpr long long SK_FLAG_BYTES = 4096;        // flags [0, G) (each reset by its consumer), error word at [1023] (sticky)
 static_assert(DP_GEMM_WS_ERROR_OFFSET == 4 * 1023, "error word offset (dp_mi355x.h)");
 constexpr int SK_MAX_WG = 256;
 
@@ -1251,6 +1250,10 @@ __global__ void __launch_bounds__(512, 1) gemm_sk_kernel(const GemmP p, const Sk
           break;
         }
       }
+      // consumed: back to 0, so every flag is 0 again when the launch ends (no per-launch
+      // clearing; a memset node of a replayed HIP graph raced the next launch's polls and let
+      // an owner add the previous replay's partials -- found by tools/parity_probe.py)
+      __hip_atomic_store(s.flags + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1305,8 +1308,6 @@ int launch_sk(const GemmP& p0, bool conv, void* ws, hipStream_t st) {
   const int G = sk_grid(p);
   s.flags = (uint32_t*)ws;
   s.part = (float*)((char*)ws + SK_FLAG_BYTES);
-  hipError_t e = hipMemsetAsync(ws, 0, SK_CLEAR_BYTES, st);
-  if (e != hipSuccess) return (int)e;
   dim3 grid(G);
   const bool rowld = p.R1 || p.R2 || p.pos || p.accumulate;
 #define DP_SK(C_, R_, L_) hipLaunchKernelGGL((gemm_sk_kernel<K_, C_, R_, L_>), grid, dim3(512), 0, st, p, s)

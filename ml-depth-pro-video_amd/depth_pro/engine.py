@@ -301,6 +301,13 @@ class Engine:
         # FOV encoder + head beside the decoder instead of the patch encoder (measured: 0.3 ms
         # slower on MI355X, so off by default; DP_FOV_LATE=1 to try)
         self.fov_late = os.environ.get("DP_FOV_LATE", "0") == "1"
+        # where the image (+ FOV) encoders run (A/B switch, DP_SIDE_MODE):
+        #   concurrent -- side stream beside the patch encoder (default);
+        #   serial     -- main stream, ahead of the patch encoder;
+        #   late       -- side stream beside the project/upsample chain, after the patch encoder
+        self.side_mode = os.environ.get("DP_SIDE_MODE", "concurrent")
+        if self.side_mode not in ("concurrent", "serial", "late"):
+            raise DPError(f"DP_SIDE_MODE={self.side_mode!r}")
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
@@ -446,17 +453,24 @@ class Engine:
         main = torch.cuda.current_stream(self.dev)
         side_ok = "side" not in _ABLATE
         ops.patchify_pyramid(self.x0, self.cols)
-        if self.serial_side:
-            self._image_encoder()
-            if self.use_fov:
-                self._fov_encoder()
-        else:
+        serial = self.serial_side or self.side_mode == "serial"
+        fov_side = self.use_fov and self.fov_late and not serial
+
+        def side_encoders():
+            if serial:
+                self._image_encoder()
+                if self.use_fov:
+                    self._fov_encoder()
+                return
             self.side.wait_stream(main)
             with torch.cuda.stream(self.side), ops.use_workspace(self.ws_side):
                 if side_ok:
                     self._image_encoder()
-                    if self.use_fov and not self.fov_late:
+                    if self.use_fov and not fov_side:
                         self._fov_encoder()
+
+        if self.side_mode != "late" or serial:
+            side_encoders()
         vp = self.vp
         if len(self.patch_groups) == 1:
             hooks = {
@@ -469,6 +483,8 @@ class Engine:
         ops.merge_windows(vp.out, 0, 5, 3, self.f0)
         ops.merge_windows(vp.out, 25, 3, 6, self.f1)
         ops.merge_windows(vp.out, 34, 1, 0, self.f2)
+        if self.side_mode == "late" and not serial:
+            side_encoders()
         # project / upsample (encoder.py:314-324)
         e = "encoder."
         ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
@@ -484,12 +500,11 @@ class Engine:
         self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
         ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
-        if not self.serial_side:
+        if not serial:
             main.wait_stream(self.side)  # join: image-encoder half of `cat` and fov tokens ready
         ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
         self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)
-        fov_side = self.use_fov and self.fov_late and not self.serial_side
         if self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
             self._fov_head()
         elif fov_side:
@@ -565,7 +580,7 @@ class Engine:
         self._err_ev = None
         if int(self._err_host.abs().sum()) != 0:
             self._err_host.zero_()
-            for w in self._err_dev:
-                w.zero_()
+            for w in [self.ws_main, self.ws_side] + self.ws_groups:
+                w.zero_()   # error word, and any hand-off flag the timed-out launch left set
             raise DPError("dp_gemm stream-K: a partial-tile hand-off timed out; the depth map of a recent "
                           "frame is invalid (workspace error word set)")

@@ -231,3 +231,39 @@ def test_patch_window_groups_match_single_group(model, groups):
         assert torch.equal(cg, c1) and torch.equal(fg, f1)
     finally:
         e.set_patch_groups(n0)
+
+
+@pytest.mark.parametrize("side_mode", ["serial", "concurrent"])
+def test_graph_replays_of_other_frames_then_frame0_match_eager(model, side_mode):
+    """Regression: replaying the captured forward on frames 1-3 and then frame 0 must give the
+    eager frame-0 result bit for bit.  With the stream-K flags cleared by a memset node, a
+    replay could absorb the previous replay's split-K partials (decoder 48^2 projection,
+    tools/parity_probe.py, serial side mode); the flags are now reset by their consumers."""
+    m, transform = model
+    e = m.engine()
+    xs = [transform(frame(k)) for k in range(4)]
+    old_mode, old_graph = e.side_mode, e.graph
+    try:
+        e.side_mode = side_mode
+        m.infer(xs[0])
+        ref = e.canonical.clone()
+        e.capture_graph()
+        for _ in range(3):
+            for k in (1, 2, 3):
+                ops_resize(xs[k], e)
+                e.run()
+        ops_resize(xs[0], e)
+        e.run()
+        torch.cuda.synchronize()
+        d = (e.canonical - ref).abs().max().item()
+        print(f"\n[{m.tag}] {side_mode}: graph frame 0 after other frames vs eager: max|d| {d:.3e}")
+        assert torch.equal(e.canonical, ref)
+        e.check_status(block=True)
+    finally:
+        e.side_mode, e.graph = old_mode, old_graph
+
+
+def ops_resize(x3, e):
+    from depth_pro import ops
+
+    ops.resize_bilinear(x3, e.x0)
