@@ -321,12 +321,16 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   }
 }
 
+
 }  // namespace
 
 extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
                             int32_t head_dim, float scale, int32_t dtype, dp_stream_t stream) {
   if (!qkv || !out) return DP_ERR_ARG;
   if (batch <= 0 || seq <= 0 || heads <= 0 || head_dim != HD) return DP_ERR_SHAPE;
+  // Measured and rejected (35 x 577): two independent 32-query sub-blocks per wave (K / V
+  // fragments shared, 210 VGPRs, 2 workgroups per CU) 98-101 us vs 75-76 us here -- the
+  // occupancy (4 workgroups / 16 waves per CU) hides more than the in-wave ILP adds.
   const int nq = (seq + QB - 1) / QB;
   if ((long long)nq * heads * batch > 0x7fffffffLL) return DP_ERR_SHAPE;
   dim3 grid(nq * heads * batch);
