@@ -1608,6 +1608,10 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       const long long cost256 = (tiles256 + ncu - 1) / ncu * 256 * 20, cost320 = (tiles320 + ncu - 1) / ncu * 320 * 20;
       const long long cost128 = (tiles128 + ncu - 1) / ncu * 128 * 23;
       if (cost128 < cost256 && cost128 < cost320) tile = DP_TILE_BIG_256x128;
+      // Measured and rejected (round 2): the 320 x 256 engine for the 768^2 ResidualBlock convs
+      // (bias-only conv in isolation 648 vs 740 us, but the ReLU-prologue + residual variants
+      // in-frame: eager conv total 5.61-5.71 -> 5.83-5.88 ms); fc1 on 320 x 256 (ties, below):
+      // frame 24.50-24.54 vs 24.62-24.67 ms, within the box's noise.
       // ties (fc1: 4 rounds of 320 rows = 5 of 256) stay on the 8-phase engine: the
       // 320 x 256 engine is 6 % faster on fc1 in isolation (205 vs 217 us) but equal
       // in-frame (199-203 us both, profiles/r01s_fc1_engine_ab/)
