@@ -301,6 +301,9 @@ class Engine:
         # FOV encoder + head beside the decoder instead of the patch encoder (measured: 0.3 ms
         # slower on MI355X, so off by default; DP_FOV_LATE=1 to try)
         self.fov_late = os.environ.get("DP_FOV_LATE", "0") == "1"
+        # Measured and rejected: the side encoders' fc2 (M = 577, K = 4096, 24 workgroups) as 2 / 4
+        # accumulating K-slice launches, to shorten the workgroups that block the patch
+        # encoder's CUs: frame 24.32 -> 24.67 / 25.41 ms.
         # where the image (+ FOV) encoders run (A/B switch, DP_SIDE_MODE):
         #   concurrent -- side stream beside the patch encoder (default);
         #   serial     -- main stream, ahead of the patch encoder;

@@ -133,9 +133,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          row_group: int = 0, row_group_out: int = 0, row_off: int = 0,
          head_w: Optional[torch.Tensor] = None, head_b: float = 0.0,
          head_corr: Optional[torch.Tensor] = None,
-         A_off: int = 0, C_off: int = 0, tile: int = 0, workspace: Optional[torch.Tensor] = None,
+         A_off: int = 0, C_off: int = 0, B_off: int = 0, tile: int = 0,
+         workspace: Optional[torch.Tensor] = None,
          plan_only: bool = False):
-    """dp_gemm. `A_off`/`C_off` are element offsets into A / C (sub-views).
+    """dp_gemm. `A_off`/`B_off`/`C_off` are element offsets into A / B / C (sub-views, e.g. a
+    K slice of a split-K GEMM: A_off = B_off = k0 with lda / ldb the full row lengths).
 
     `workspace` (or the one set by `use_workspace`) enables the stream-K engine.
     `plan_only=True` launches nothing and returns (tile, workgroups) from dp_gemm_plan.
@@ -145,7 +147,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     a.dtype = dtype_code(B.dtype)
     a.A = A.data_ptr() + A_off * A.element_size()
     a.lda = K if lda is None else lda
-    a.B = B.data_ptr()
+    a.B = B.data_ptr() + B_off * B.element_size()
     a.ldb = K if ldb is None else ldb
     if conv is not None:
         a.a_mode = DP_A_CONV
@@ -187,13 +189,13 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
         t, g = ctypes.c_int32(), ctypes.c_int32()
         check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
         return t.value, g.value
-    _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None)
+    _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None, B_off)
     kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
     with _Timed(kind, 2.0 * M * N * K, (M, N, K), B.dtype):
         check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
 
 
-def _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head, head_ps) -> None:
+def _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head, head_ps, B_off=0) -> None:
     """Host-side bounds check: every element dp_gemm will read or write lies inside the
     tensors passed (a wrong leading dimension would otherwise write past the buffer on
     the GPU)."""
@@ -206,7 +208,7 @@ def _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head, head_ps) -
         need(A, A_off, (M // (a.out_h * a.out_w)) * a.in_h * a.in_w * a.in_c, "A (conv input)")
     else:
         need(A, A_off, (M - 1) * a.lda + K, "A")
-    need(B, 0, (N - 1) * a.ldb + K, "B")
+    need(B, B_off, (N - 1) * a.ldb + K, "B")
     if head_ps:
         need(C, C_off, (M // (a.out_h * a.out_w)) * 4 * a.out_h * a.out_w, "C (pixel-shuffle head)")
     elif head:
