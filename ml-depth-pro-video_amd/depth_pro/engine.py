@@ -27,7 +27,7 @@ from ._lib import DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DPError, lo
 from .spec import DEPTH, EMBED_DIM, HEADS, IMG_SIZE, MLP_DIM, TOKENS
 
 # Timing ablations for tools/frame_ablation.py only (results are wrong when set):
-# comma list of {side, attn, ln, vitgemm, decoder, head}.
+# comma list of {side, img, fovenc, attn, ln, vitgemm, decoder, head}.
 _ABLATE = set(filter(None, os.environ.get("DP_ABLATE", "").split(",")))
 
 NWIN = 35
@@ -315,12 +315,16 @@ class Engine:
         # fuse_lowres waits for the image encoder alone: 24.41-24.43 -> 24.16-24.25 ms per frame
         # (DP_SIDE_STREAMS=1: both encoders on one side stream)
         self.side_streams = int(os.environ.get("DP_SIDE_STREAMS", "2"))
+        # GEMM engine of the side encoders' block GEMMs (DP_SIDE_TILE, a DP_TILE_* value; 0 = planner)
+        self.side_tile = int(os.environ.get("DP_SIDE_TILE", "0"))
         if self.side_mode not in ("concurrent", "serial", "late"):
             raise DPError(f"DP_SIDE_MODE={self.side_mode!r}")
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
         P, M = self.P, n_img * TOK
+        # side encoders (one image, M = 577): engine choice for CU-time, not latency (DP_SIDE_TILE)
+        t = self.side_tile if n_img == 1 else 0
         # patch embed (k16 s16 conv as GEMM over the im2col rows) + bias + pos -> rows 1..576
         ops.gemm(self.cols, P[pre + "pe.w"], buf.x, M=n_img * PTOK, N=D, K=768,
                  A_off=cols_off_rows * 768, bias=P[pre + "pe.b"], pos=P[pre + "pos"], ldpos=D,
@@ -331,19 +335,20 @@ class Engine:
             if "ln" not in _ABLATE:
                 ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
             if "vitgemm" not in _ABLATE:
-                ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"])
+                ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"],
+                         tile=t)
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS)
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
-                         gamma=P[b + "ls1.gamma"], accumulate=True)
+                         gamma=P[b + "ls1.gamma"], accumulate=True, tile=t)
             if "ln" not in _ABLATE:
                 ops.layernorm(buf.x, P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, M, D)
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
-                         act=DP_ACT_GELU)
+                         act=DP_ACT_GELU, tile=t)
                 ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
-                         gamma=P[b + "ls2.gamma"], accumulate=True)
+                         gamma=P[b + "ls2.gamma"], accumulate=True, tile=t)
             if hooks and i in hooks:
                 hooks[i]()
         ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
@@ -473,14 +478,15 @@ class Engine:
                 return
             self.side.wait_stream(main)
             with torch.cuda.stream(self.side), ops.use_workspace(self.ws_side):
-                if side_ok:
+                if side_ok and "img" not in _ABLATE:
                     self._image_encoder()
+                if side_ok:
                     if self.use_fov and not fov_side and self.side_streams == 1:
                         self._fov_encoder()
             if self.use_fov and not fov_side and self.side_streams == 2:
                 self.side2.wait_stream(main)
                 with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
-                    if side_ok:
+                    if side_ok and "fovenc" not in _ABLATE:
                         self._fov_encoder()
 
         if self.side_mode != "late" or serial:
