@@ -27,6 +27,7 @@
 namespace {
 
 constexpr int BK = 64;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 struct GemmP {
   int M, N, K;
@@ -58,6 +59,7 @@ struct GemmP {
   const float* head_corr;
   int tiles_n, tiles_m;
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
+  unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
 };
 
 // Process-wide ablation / fault-injection bits, set only by dp_gemm_debug_flags (tools and
@@ -384,6 +386,78 @@ __device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc
       o.z = (uint32_t)K_::from_f(x[4]) | ((uint32_t)K_::from_f(x[5]) << 16);
       o.w = (uint32_t)K_::from_f(x[6]) | ((uint32_t)K_::from_f(x[7]) << 16);
       *(uint4*)((u16*)p.C + off[it]) = o;
+    }
+  }
+}
+
+// epilogue_rows for the persistent engine: the same arithmetic, C written with buffer stores
+// that EVERY lane issues -- rows past M (or columns past N) get the out-of-range offset
+// c_bytes and are dropped -- so the number of stores per tile is a compile-time constant
+// the engine's counted vmcnt relies on.  DP_STORE_ROWS only.
+template <typename K_, int NIT>
+__device__ __forceinline__ void epilogue_rows_buf(const GemmP& p, const ColConst& cc, const int (&ms)[NIT], int n,
+                                                  float (&v)[NIT][8], __amdgpu_buffer_rsrc_t crs, int esz) {
+  const int nc = n < p.N ? n : p.N - 8;
+  int mc[NIT];
+  long long off[NIT];
+  #pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    mc[it] = ms[it] < p.M ? ms[it] : p.M - 1;
+    off[it] = out_offset(p, mc[it], nc);
+  }
+  uint4 r1[NIT], r2[NIT];
+  float4 c0[NIT], c1[NIT];
+  if (p.R1) {
+    #pragma unroll
+    for (int it = 0; it < NIT; ++it) r1[it] = *(const uint4*)(p.R1 + (long long)mc[it] * p.ldr1 + nc);
+  }
+  if (p.R2) {
+    #pragma unroll
+    for (int it = 0; it < NIT; ++it) r2[it] = *(const uint4*)(p.R2 + (long long)mc[it] * p.ldr2 + nc);
+  }
+  const bool acc32 = p.accumulate && p.c_dtype == DP_F32;
+  if (acc32) {
+    #pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const float* c = (const float*)p.C + off[it];
+      c0[it] = *(const float4*)c;
+      c1[it] = *(const float4*)(c + 4);
+    }
+  }
+  const bool nok = n < p.N;
+  #pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    float (&x)[8] = v[it];
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] += cc.b[r];
+    if (p.act == DP_ACT_RELU) {
+      #pragma unroll
+      for (int r = 0; r < 8; ++r) x[r] = fmaxf(x[r], 0.f);
+    } else if (p.act == DP_ACT_GELU) {
+      #pragma unroll
+      for (int r = 0; r < 8; ++r) x[r] = gelu_erf(x[r]);
+    }
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) x[r] *= cc.g[r];
+    if (p.pos) add8_f32(x, p.pos + (long long)(mc[it] % p.pos_group + p.pos_off) * p.ldpos + nc);
+    if (p.R1) add8_u4<K_>(x, r1[it]);
+    if (p.R2) add8_u4<K_>(x, r2[it]);
+    if (acc32) {
+      x[0] += c0[it].x; x[1] += c0[it].y; x[2] += c0[it].z; x[3] += c0[it].w;
+      x[4] += c1[it].x; x[5] += c1[it].y; x[6] += c1[it].z; x[7] += c1[it].w;
+    }
+    const unsigned bo = (nok && ms[it] < p.M) ? (unsigned)(off[it] * esz) : p.c_bytes;
+    if (p.c_dtype == DP_F32) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, f32x4_t{x[0], x[1], x[2], x[3]}), crs, bo, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, f32x4_t{x[4], x[5], x[6], x[7]}), crs,
+                                             bo == p.c_bytes ? bo : bo + 16, 0, 0);
+    } else {
+      u32x4_t o;
+      o[0] = (uint32_t)K_::from_f(x[0]) | ((uint32_t)K_::from_f(x[1]) << 16);
+      o[1] = (uint32_t)K_::from_f(x[2]) | ((uint32_t)K_::from_f(x[3]) << 16);
+      o[2] = (uint32_t)K_::from_f(x[4]) | ((uint32_t)K_::from_f(x[5]) << 16);
+      o[3] = (uint32_t)K_::from_f(x[6]) | ((uint32_t)K_::from_f(x[7]) << 16);
+      __builtin_amdgcn_raw_buffer_store_b128(o, crs, bo, 0, 0);
     }
   }
 }
@@ -835,6 +909,202 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   DP_STAMP_SAVE(wgid);
 }
 
+
+// ============================================== persistent data-parallel big engine
+// gemm_big_kernel's K loop (2-stage ring, one barrier per K step, all A fragments of a
+// sub-step read up front) inside a tile loop: min(tiles, CUs) workgroups walk tiles
+// wgid, wgid + G, ...  At the last K step of a tile the FIRST K step of the next tile is
+// issued into the stage just freed, so its LDS-DMA runs under the epilogue; the epilogue
+// stages through the stage it just computed from and writes C with buffer stores that
+// every lane issues (rows past M get an out-of-range offset: dropped by the hardware),
+// so the next tile's first wait can be a COUNTED vmcnt that lets this tile's stores
+// drain under its K loop instead of a per-round dispatch + prologue + store drain.
+// Store modes: rows (incl. row-group remap), no fused head.
+// ROWLD: the epilogue reads per-row operands (residuals, pos, the fp32 C being accumulated
+// into); without them it needs fewer VGPRs (the 320 x 256 tile is at the 256 limit).
+template <typename K_, int BM, int BN, bool CONV, bool RELU, bool ROWLD>
+__global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
+  constexpr int BKT = 64, WN = 4, WM = 2;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int LA = BM / 64, LB = BN / 64;
+  constexpr int SROW = TN + 4;                                   // fp32 staging row stride
+  constexpr int PR = 8 * 32 * SROW * 4 <= STAGE ? 32 : 16;       // staged rows per pass per wave
+  constexpr int CPR = TN / 8, RPI = 64 / CPR, NIT = PR / RPI;
+  constexpr int STORES = (FM * 16 / PR) * NIT;                   // 16-B stores per lane per tile (16-bit C)
+  static_assert(8 * PR * SROW * 4 <= STAGE && FM % (PR / 16) == 0 && NIT % 2 == 0, "staging");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave / WN, wn = wave % WN;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int T = p.tiles_m * p.tiles_n;
+  if (wgid >= T) return;
+  // this workgroup's tiles are wgid, wgid + G, ...: at any moment the workgroups of one XCD
+  // (consecutive wgids) work on consecutive tiles of the band raster, as the rounds of the
+  // data-parallel launch do (shared A / B panels in that XCD's L2)
+  const int t_begin = wgid;
+
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  // 32-bit element offsets from the (uniform) A / B bases instead of 64-bit pointers: they
+  // stay live through the epilogue (the next tile's loads are in flight), so they are kept
+  // small (the host guarantees M * lda and N * ldb < 2^31)
+  int a_off[LA];
+  ConvRow a_cr[LA];
+  int b_off[LB];
+  auto setup = [&](int m0, int n0) {
+    #pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int m = m0 + i * 64 + prow;
+      if constexpr (CONV) a_cr[i] = conv_row(p, m);
+      else a_off[i] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
+    }
+    #pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int n = n0 + i * 64 + prow;
+      b_off[i] = (n < p.N ? n : p.N - 1) * (int)p.ldb + pchunk * 8;
+    }
+  };
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
+  auto issue = [&](int kt, int stage) {
+    const uint32_t sa = lds_base + stage * STAGE;
+    const uint32_t sb = sa + A_BYTES;
+    const int k0 = kt * BKT;
+    int t_ky = 0, t_kx = 0, t_ci = 0;
+    if constexpr (CONV) conv_tap(p, k0, t_ky, t_kx, t_ci);
+    #pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const void* src;
+      if constexpr (CONV) {
+        bool inb;
+        const u16* s = conv_src(p, a_cr[i], t_ky, t_kx, t_ci + pchunk * 8, inb);
+        src = inb ? (const void*)s : (const void*)g_zero_page;
+      } else {
+        src = p.A + (a_off[i] + k0);
+      }
+      glds16(src, sa + i * 8192);
+    }
+    #pragma unroll
+    for (int i = 0; i < LB; ++i) glds16(p.B + (b_off[i] + k0), sb + i * 8192);
+  };
+
+  f32x4_t acc[FM][FN];
+  const int frow = lane & 15, fchunk = lane >> 4;
+  auto compute = [&](int stage) {
+    const u16* sa = (const u16*)(smem + stage * STAGE);
+    const u16* sb = (const u16*)(smem + stage * STAGE + A_BYTES);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 bf[FN];
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *(const uint4*)(sb + lds_off_t<BKT>(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      // A fragments read up front in groups of FA (all FM for the 256-row tile; two halves
+      // for the 320-row tile, whose persistent state leaves no room for ten)
+      constexpr int FA = FM > 8 ? FM / 2 : FM;
+      #pragma unroll
+      for (int i0 = 0; i0 < FM; i0 += FA) {
+        uint4 afs[FA];
+        #pragma unroll
+        for (int i = 0; i < FA; ++i)
+          afs[i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + (i0 + i) * 16 + frow, ks * 4 + fchunk));
+        __builtin_amdgcn_s_setprio(1);
+        #pragma unroll
+        for (int i = 0; i < FA; ++i) {
+          uint4 af = afs[i];
+          if constexpr (RELU) af = relu_pk16(af);
+          #pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i0 + i][j] = K_::mfma16(bf[j], af, acc[i0 + i][j]);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  };
+
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void*)p.C, (short)0, (int)p.c_bytes, 0x00020000);
+  const int esz = p.c_dtype == DP_F32 ? 4 : 2;
+  const int KT = p.K / BKT;
+  int tm, tn;
+  tile_coords(p, t_begin, tm, tn);
+  int m0 = tm * BM, n0 = tn * BN;
+  setup(m0, n0);
+  issue(0, 0);
+  int stage = 0;
+  for (int t = t_begin;; ) {
+    #pragma unroll
+    for (int i = 0; i < FM; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const bool has_next = t + G < T;
+    int m0n = 0, n0n = 0;
+    for (int kt = 0; kt < KT; ++kt) {
+      // step 0 of a later tile: only its own DMA (issued before the previous epilogue's
+      // STORES stores) has to have landed; the stores may still be draining
+      if (kt == 0 && t != t_begin) wait_vmcnt<STORES>();
+      else wait_vmcnt<0>();
+      lds_barrier();
+      if (kt + 1 < KT) {
+        issue(kt + 1, stage ^ 1);
+      } else if (has_next) {
+        tile_coords(p, t + G, tm, tn);
+        m0n = tm * BM;
+        n0n = tn * BN;
+        setup(m0n, n0n);
+        issue(0, stage ^ 1);
+      }
+      compute(stage);
+      stage ^= 1;
+    }
+    // epilogue of tile t, staged through the stage just computed from (stage ^ 1)
+    lds_barrier();
+    float* stg = (float*)(smem + (stage ^ 1) * STAGE) + wave * (PR * SROW);
+    const int c8 = (lane % CPR) * 8, n_l = n0 + wn * TN + c8;
+    ColConst cc;
+    load_colconst(p, n_l, cc);
+    #pragma unroll
+    for (int q = 0; q < FM * 16 / PR; ++q) {
+      #pragma unroll
+      for (int i = 0; i < PR / 16; ++i)
+        #pragma unroll
+        for (int j = 0; j < FN; ++j)
+          *(f32x4_t*)(stg + (i * 16 + (lane & 15)) * SROW + j * 16 + 4 * (lane >> 4)) = acc[q * (PR / 16) + i][j];
+      #pragma unroll
+      for (int c0 = 0; c0 < NIT; c0 += 2) {
+        float v[2][8];
+        int ms[2];
+        #pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int row = (c0 + it) * RPI + lane / CPR;
+          const f32x4_t lo = *(const f32x4_t*)(stg + row * SROW + c8);
+          const f32x4_t hi = *(const f32x4_t*)(stg + row * SROW + c8 + 4);
+          #pragma unroll
+          for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
+          ms[it] = m0 + wm * TM + q * PR + row;
+        }
+        if constexpr (ROWLD) {
+          epilogue_rows_buf<K_, 2>(p, cc, ms, n_l, v, crs, esz);
+        } else {
+          GemmP q = p;
+          q.R1 = nullptr; q.R2 = nullptr; q.pos = nullptr; q.accumulate = 0;
+          epilogue_rows_buf<K_, 2>(q, cc, ms, n_l, v, crs, esz);
+        }
+      }
+      // the next pass rewrites this wave's slab: its reads of this pass are done first
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (!has_next) break;
+    t += G;
+    m0 = m0n;
+    n0 = n0n;
+  }
+}
+
 // ======================================================= 8-phase 256x256 engine
 // 256 x 256 x 64 tile, 8 waves (2 x 4, wave tile 128 x 64), K loop cut into 4
 // phases per K tile -- one 64 x 32 C quadrant x K 64 = 16 MFMAs per wave per
@@ -1055,7 +1325,6 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
 // spin is bounded (a timeout sets an error word instead of hanging the GPU).
 // The epilogue stages 16-row slices through its own 32 KiB of LDS so that the
 // 128 KiB ring stays live underneath it.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 constexpr int SK_A_BYTES = 256 * 128;            // 256 rows x 64 16-bit
 constexpr int SK_STAGE = 2 * SK_A_BYTES;         // A + B
 constexpr int SK_RING = 2 * SK_STAGE;            // 2 stages: 128 KiB
@@ -1499,9 +1768,38 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   return 0;
 }
 
+template <typename K_, int BM, int BN>
+int launch_pbig(const GemmP& p0, bool conv, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.tiles_m = (p.M + BM - 1) / BM;
+  const int T = p.tiles_n * p.tiles_m;
+  int G = num_cus();
+  if (G > T) G = T;
+  dim3 grid(G);
+  const bool rowld = p.R1 || p.R2 || p.pos || p.accumulate;
+#define DP_PB(C_, R_, L_) hipLaunchKernelGGL((gemm_pbig_kernel<K_, BM, BN, C_, R_, L_>), grid, dim3(NT_BIG), 0, s, p)
+  if (rowld) {
+    if (conv && p.relu_a) DP_PB(true, true, true);
+    else if (conv) DP_PB(true, false, true);
+    else if (p.relu_a) DP_PB(false, true, true);
+    else DP_PB(false, false, true);
+  } else {
+    if (conv && p.relu_a) DP_PB(true, true, false);
+    else if (conv) DP_PB(true, false, false);
+    else if (p.relu_a) DP_PB(false, true, false);
+    else DP_PB(false, false, false);
+  }
+#undef DP_PB
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename K_>
 int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
   switch (tile) {
+    case DP_TILE_PBIG_320x256: return launch_pbig<K_, 320, 256>(p, conv, s);
+    case DP_TILE_PBIG_256x256: return launch_pbig<K_, 256, 256>(p, conv, s);
     case DP_TILE_256x64: return launch_small<K_, 256, 64, 4, 1>(p, conv, s);
     case DP_TILE_256x32: return launch_small<K_, 256, 32, 4, 1>(p, conv, s);
     case DP_TILE_128x128: return launch_small<K_, 128, 128, 2, 2>(p, conv, s);
@@ -1619,6 +1917,32 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       else tile = (tiles256 >= 600 && a->a_mode != DP_A_CONV) ? DP_TILE_8PH_256x256 : DP_TILE_BIG_256x256;
     }
   }
+  // byte extent of C for the persistent engine's bounded buffer stores (0: not eligible)
+  unsigned c_bytes = 0;
+  if (a->store_mode == DP_STORE_ROWS && !a->head_w) {
+    long long last = a->M - 1;
+    if (a->row_group) last = (last / a->row_group) * a->row_group_out + a->row_off + last % a->row_group;
+    const long long ext = (last * a->ldc + a->N) * (a->c_dtype == DP_F32 ? 4 : 2);
+    if (ext < 0xFFFFFF00LL) c_bytes = (unsigned)ext;
+  }
+  // the persistent engine keeps 32-bit operand offsets
+  if (a->a_mode == DP_A_DENSE && (long long)a->M * a->lda >= (1LL << 31)) c_bytes = 0;
+  if ((long long)a->N * a->ldb >= (1LL << 31)) c_bytes = 0;
+  if ((tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) && (!c_bytes || a->N % 256)) return DP_ERR_ARG;
+  // Multi-round GEMMs on the 320 x 256 / 256 x 256 engines (the ViT qkv: 768 tiles, the
+  // 768^2 decoder convs: 2304) run persistent: the next tile's first K step loads under
+  // each epilogue and the stores drain under the next K loop.  Debug flag 1024: off.
+  if (a->tile == DP_TILE_AUTO && c_bytes && !(dbg & 1024)) {
+    const long long ncu = num_cus();
+    // dense (ViT) GEMMs only with debug 2048: they run beside the side encoders, and a
+    // persistent grid whose workgroups cannot all start at once ends on a tail (qkv: 146 ->
+    // 140 us alone, frame 23.74 -> 23.89 ms in-frame)
+    const bool dense_ok = a->a_mode == DP_A_CONV || (dbg & 2048);
+    if (dense_ok && tile == DP_TILE_BIG_320x256 && (long long)((a->M + 319) / 320) * (a->N / 256) >= 2 * ncu)
+      tile = DP_TILE_PBIG_320x256;
+    else if (dense_ok && tile == DP_TILE_BIG_256x256 && tiles256 >= 2 * ncu)
+      tile = DP_TILE_PBIG_256x256;
+  }
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
 
   p.M = a->M; p.N = a->N; p.K = a->K;
@@ -1641,6 +1965,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     p.tiles_m = (a->M + 255) / 256;
   }
   p.dbg = dbg;
+  p.c_bytes = c_bytes;
   return 0;
 }
 }  // namespace
@@ -1659,10 +1984,13 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
     case DP_TILE_BIG_256x128: case DP_TILE_BIG_256x128_K32: case DP_TILE_DEEP_256x128: bn = 128; break;
     case DP_TILE_BIG_320x256: bm = 320; bn = 256; break;
     case DP_TILE_BIG_512x128: bm = 512; bn = 128; break;
+    case DP_TILE_PBIG_320x256: bm = 320; bn = 256; break;
     default: bn = 256;
   }
   if (tile_out) *tile_out = tile;
-  if (grid_out) *grid_out = tile == DP_TILE_STREAMK_256x256 ? sk_grid(p) : ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  int grid = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  if (tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) grid = grid < num_cus() ? grid : num_cus();
+  if (grid_out) *grid_out = tile == DP_TILE_STREAMK_256x256 ? sk_grid(p) : grid;
   return 0;
 }
 

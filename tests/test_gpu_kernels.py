@@ -408,3 +408,50 @@ def test_gemm_stream_k_timeout_sets_sticky_error_word(cuda):
     assert ops.workspace_error(ws) != 0
     ops.gemm(A, B, C, M=M, N=N, K=K, tile=DP_TILE_STREAMK_256x256, workspace=ws)   # clean launch
     assert ops.workspace_error(ws) != 0, "error word must be sticky across launches"
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("pair", ["320", "256"])
+@pytest.mark.parametrize("case", ["dense_bias", "gelu_ragged", "acc_f32", "conv_relu_res", "rowgroup"])
+def test_persistent_engine_bit_identical_to_data_parallel(cuda, dt, pair, case):
+    """The persistent big engine (DP_TILE_PBIG_*: tile loop, next tile's first K step under the
+    epilogue, bounded buffer stores) computes every tile exactly as the data-parallel engine:
+    bit-identical C, including ragged last tiles (dropped out-of-range stores) and the fp32
+    accumulate / residual / row-group-remap epilogues."""
+    from depth_pro._lib import DP_TILE_PBIG_256x256, DP_TILE_PBIG_320x256
+
+    tp, tb = (DP_TILE_PBIG_320x256, DP_TILE_BIG_320x256) if pair == "320" else (DP_TILE_PBIG_256x256,
+                                                                                  DP_TILE_BIG_256x256)
+    g = torch.Generator().manual_seed(sum(map(ord, case)))
+    kw = {}
+    if case == "conv_relu_res":
+        S, C = 96, 256
+        A = rnd(S * S, C, dt=dt, dev=cuda, gen=g)
+        M, N, K = S * S, 256, 9 * C
+        kw = dict(conv=dict(in_h=S, in_w=S, in_c=C, k=3, stride=1, pad=1, out_h=S, out_w=S), relu_a=True,
+                  R1=rnd(M, N, dt=dt, dev=cuda, gen=g), ldr1=N, R2=rnd(M, N, dt=dt, dev=cuda, gen=g), ldr2=N)
+    else:
+        M, N, K = {"dense_bias": (20195, 3072, 1024), "gelu_ragged": (4999, 1536, 512),
+                   "acc_f32": (3001, 1024, 2048), "rowgroup": (35 * 576, 1024, 768)}[case]
+        A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    kw.update(bias=bias)
+    if case == "gelu_ragged":
+        kw.update(act=DP_ACT_GELU)
+    rows = M
+    if case == "rowgroup":   # patch-embed remap: 576 rows per window -> 577 with a cls row in front
+        kw.update(row_group=576, row_group_out=577, row_off=1)
+        rows = 35 * 577
+    if case == "acc_f32":
+        kw.update(gamma=torch.rand(N, generator=g).to(cuda), accumulate=True)
+        C0 = torch.randn(rows, N, generator=g).to(cuda)
+        C1, C2 = C0.clone(), C0.clone()
+    else:
+        cdt = torch.float32 if case == "rowgroup" else dt
+        C1 = torch.full((rows, N), 7.0, dtype=cdt, device=cuda)
+        C2 = C1.clone()
+    ops.gemm(A, B, C1, M=M, N=N, K=K, tile=tp, **kw)
+    ops.gemm(A, B, C2, M=M, N=N, K=K, tile=tb, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2), (C1.float() - C2.float()).abs().max().item()
