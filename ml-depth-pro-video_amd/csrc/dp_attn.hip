@@ -14,8 +14,9 @@
 // (row >> 1) & 7 (conflict-free ds_read_b128 of 16 rows), V by 64-B halves on odd
 // row pairs, read transposed with ds_read_b64_tr_b16 (conflict-free).  Q stays in
 // registers; 4 workgroups (16 waves) per CU.
-// Softmax: scale folded into one FMA per score, exp2, a deferred running-max
-// rescale, and row sums taken by the matrix core (an all-ones V^T block).
+// Softmax in log2 units: one FMA + exp2 per score against a running max that only the
+// first half key tile sets (an overflow, checked once at the end, sends the workgroup
+// through an exact per-tile-max pass), VALU row sums.
 // A last, partial key tile is masked and skips its empty 32-key half; one or two
 // leftover keys (the ViT's 577 = 9 x 64 + 1) go through the VALU instead (tail_key).
 #include <cstdlib>
@@ -56,12 +57,20 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
       : "memory");
 }
 
+// Running max (m_run, log2 units).  LAZY: set exactly by the first 32-key half tile
+// only; every later score is taken as P = 2^(s sl2 - m_run) with no max pass, no
+// compare and no rescale.  P only has to stay representable (16-bit B operand, fp32
+// sums), and a later key beyond that range (> ~127 log2 units above the first half
+// tile's max for bf16, > ~16 for f16) makes the row sum or O non-finite: the workgroup
+// then runs its keys again with EXACT, the per-half-tile max and deferred rescale
+// (m_run moves when exceeded by > 8, so P <= 256) -- rare on real inputs, checked once.
 // VSUM: row sums of P as f32 VALU adds (2 packed adds per 4 scores) instead of an MFMA
-// against an all-ones operand (4 of the 20 MFMAs of a tile).
-template <typename K_, bool VSUM>
+// against an all-ones operand (4 MFMAs per 64-key tile).
+template <typename K_, bool LAZY, bool VSUM>
 __global__ void __launch_bounds__(256, 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
   __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
+  __shared__ int redo;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // XCD-aware remap: workgroup i is dispatched to XCD i % 8, so consecutive work
@@ -82,6 +91,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   const int q = qblk * QB + wave * 32 + l32;
   // a wave whose 32 queries are all past seq (tail block) only helps stage K/V
   const bool active = __builtin_amdgcn_readfirstlane(qblk * QB + wave * 32) < seq;
+  if (tid == 0) redo = 0;
 
   // Q fragments (B operand of S^T = K Q^T): Q[q][16*ks + 8*hi + 0..7]
   uint4 qf[4];
@@ -101,7 +111,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   // (finite, masked to -inf / weight 0 in the partial tile).
   const int prow = wave * 8 + (lane >> 3), pslot = lane & 7;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(&smem[0][0]) + wave * 1024);
-  auto issue = [&](int k0, int buf) {
+  auto issue = [&](int k0, int buf) __attribute__((always_inline)) {
     const uint32_t dk = __builtin_amdgcn_readfirstlane(lds0 + buf * 2 * TILE_B), dv = dk + TILE_B;
     #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -116,118 +126,107 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   // O^T = V^T P^T: d block db, key step (kb, st), first/second 4-key group g2
   const int grp = lane >> 4, gi = lane & 15;
   const int tq = gi >> 2, tp = gi & 3;
-  auto vt_addr = [&](int db, int k0, int g2) {
+  auto vt_addr = [&](int db, int k0, int g2) __attribute__((always_inline)) {
     const int row = k0 + 4 * hi + 8 * g2 + tq;
     const int byte = 2 * (db * 32 + 16 * (grp & 1) + 4 * tp);
     return v_off(row, byte);
   };
 
-  f32x16_t o[2], osum;   // osum: row sums of P, from an all-ones A operand (every row equal)
-  f32x2_t lsum = {0.f, 0.f};   // VSUM: this lane's share of its query's row sum
-  #pragma unroll
-  for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; osum[i] = 0.f; }
+  f32x16_t o[2], osum;         // osum (!VSUM): row sums of P from an all-ones A operand
+  f32x2_t lsum;                // VSUM: this lane's share of its query's row sum (its 32 of 64 keys)
+  float m_run;
   const uint32_t one2 = K_::pack2(1.f, 1.f);
   const uint4 ones = make_uint4(one2, one2, one2, one2);
-  float m_run = -1e30f;
 
-  // One 64-key tile.  PARTIAL (the last tile when seq % 64 != 0): keys past seq
-  // are masked, and the second 32-key half is skipped when it holds none.
-  auto do_tile = [&](int t, auto partial_tag) {
+  auto rescale = [&](float m_upd) __attribute__((always_inline)) {   // m_run -> m_upd (>= m_run)
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_upd);
+    #pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      o[0][i] *= alpha; o[1][i] *= alpha;
+      if constexpr (!VSUM) osum[i] *= alpha;
+    }
+    if constexpr (VSUM) lsum *= alpha;
+    m_run = m_upd;
+  };
+
+  // One 32-key half (kb) of a 64-key tile: S^T = K Q^T, softmax, O^T += V^T P^T; halves go
+  // one after the other so only 16 score registers are live.  PARTIAL (the last tile when
+  // seq % 64 != 0): keys past seq are masked.  setmax: take this half tile's max (exact:
+  // every half tile, with the deferred rescale; lazy: the first one, which sets m_run).
+  // `exact` is a workgroup-uniform runtime flag, so the redo pass reuses this code.
+  auto do_half = [&](int t, int kb, auto partial_tag, bool setmax, bool exact) __attribute__((always_inline)) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
-    if (!active) return;
     const int cur = t & 1;
     const int kbase = t * KT;
     const char* K = smem[cur];
     const char* V = smem[cur] + TILE_B;
-    const bool two = !PARTIAL || kbase + 32 < seq;
-    // ---- S^T for the two 32-key blocks
-    f32x16_t s[2];
+    f32x16_t s;
     #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      if (PARTIAL && kb == 1 && !two) {
-        #pragma unroll
-        for (int i = 0; i < 16; ++i) s[1][i] = -INFINITY;
-        break;
-      }
-      #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const uint4 kf = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
-        s[kb] = K_::mfma32(kf, qf[ks], ks == 0 ? f32x16_t{} : s[kb]);
-      }
+    for (int ks = 0; ks < 4; ++ks) {
+      const uint4 kf = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
+      s = K_::mfma32(kf, qf[ks], ks == 0 ? f32x16_t{} : s);
     }
     if constexpr (PARTIAL) {
       #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-          if (key >= seq) s[kb][r] = -INFINITY;
-        }
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (key >= seq) s[r] = -INFINITY;
+      }
     }
-    // ---- online softmax (this lane's query; rows = keys)
-    float mx = fmaxf(s[0][0], s[0][1]);
-    #pragma unroll
-    for (int r = 2; r < 16; ++r) mx = fmaxf(mx, s[0][r]);
-    #pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[1][r]);
-    {
+    if (setmax) {
+      // this lane's query; its other 16 keys of the half tile are in lane ^ 32
+      float mx = fmaxf(s[0], s[1]);
+      #pragma unroll
+      for (int r = 2; r < 16; ++r) mx = fmaxf(mx, s[r]);
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
-    // Deferred rescale: the reference max m_run moves only when a row's max
-    // exceeds it by more than 8 (log2 units), so P = 2^(s - m_run) <= 256 and
-    // the O / row-sum rescale (and its exp) is skipped on most tiles.  P is
-    // rounded to 16 bits relative to its own magnitude either way.
-    const float m_new = mx * sl2;
-    if (__builtin_amdgcn_ballot_w64(m_new > m_run + 8.f)) {
-      const float m_upd = fmaxf(m_run, m_new);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_upd);
-      #pragma unroll
-      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; osum[i] *= alpha; }
-      lsum *= alpha;
-      m_run = m_upd;
-    }
-    uint4 pf[2][2];
-    #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-      #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        uint32_t w[4];
-        #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const float p0 = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * st + 2 * jj], sl2, -m_run));
-          const float p1 = __builtin_amdgcn_exp2f(fmaf(s[kb][8 * st + 2 * jj + 1], sl2, -m_run));
-          w[jj] = K_::pack2(p0, p1);
-          if constexpr (VSUM) lsum += f32x2_t{p0, p1};
-        }
-        pf[kb][st] = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-    // ---- O^T += V^T P^T
-    #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      if (PARTIAL && kb == 1 && !two) break;
-      #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int k0 = kb * 32 + 16 * st;
-        #pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 0)));
-          const v4s_t up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 1)));
-          const uint2 a = __builtin_bit_cast(uint2, lo), c = __builtin_bit_cast(uint2, up);
-          o[db] = K_::mfma32(make_uint4(a.x, a.y, c.x, c.y), pf[kb][st], o[db]);
-        }
-        if constexpr (!VSUM) osum = K_::mfma32(ones, pf[kb][st], osum);
+      const float m_new = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
+      if (exact) {
+        if (__builtin_amdgcn_ballot_w64(m_new > m_run + 8.f)) rescale(fmaxf(m_run, m_new));
+      } else {
+        m_run = m_new;   // the first half tile holds a valid key for every lane: finite
       }
     }
+    uint4 pf[2];
+    #pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      uint32_t w[4];
+      #pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj], sl2, -m_run));
+        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
+        w[jj] = K_::pack2(p0, p1);
+        if constexpr (VSUM) lsum += f32x2_t{p0, p1};
+      }
+      pf[st] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    #pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int k0 = kb * 32 + 16 * st;
+      #pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 0)));
+        const v4s_t up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 1)));
+        const uint2 a = __builtin_bit_cast(uint2, lo), c = __builtin_bit_cast(uint2, up);
+        o[db] = K_::mfma32(make_uint4(a.x, a.y, c.x, c.y), pf[st], o[db]);
+      }
+      if constexpr (!VSUM) osum = K_::mfma32(ones, pf[st], osum);
+    }
+  };
+  // a 64-key tile = two halves; the second half of a partial tile is skipped when it holds no key
+  auto do_tile = [&](int t, auto partial_tag, bool first, bool exact) __attribute__((always_inline)) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
+    if (!active) return;
+    do_half(t, 0, partial_tag, exact || first, exact);
+    if (!PARTIAL || t * KT + 32 < seq) do_half(t, 1, partial_tag, exact, exact);
   };
 
   // One leftover key (seq = 64 n + r, r <= TAIL_VALU: the ViT's 577 = 9 x 64 + 1) costs a
   // whole masked MFMA tile on the partial path; on the VALU it is a 64-d dot product per
   // query (each lane holds half of its query's dims: FMAs + one permlane32 swap), the same
   // online-softmax update, and a rank-1 update of O (p rounded to 16 bits like the MFMA path's P).
-  auto tail_key = [&](int key) {
+  auto tail_key = [&](int key) __attribute__((always_inline)) {
     const u16* kr = base + (long long)key * ldq + kcol;
     const u16* vr = base + (long long)key * ldq + vcol;
     float dot = 0.f;
@@ -247,18 +246,12 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       dot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
     }
     const float sc = dot * sl2;
-    if (__builtin_amdgcn_ballot_w64(sc > m_run + 8.f)) {
-      const float m_upd = fmaxf(m_run, sc);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_upd);
-      #pragma unroll
-      for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; osum[i] *= alpha; }
-      lsum *= alpha;
-      m_run = m_upd;
-    }
+    // m_run = -inf before any key (no MFMA tile ran): the first key always sets it
+    if (__builtin_amdgcn_ballot_w64(sc > m_run + 8.f)) rescale(fmaxf(m_run, sc));
     const float pr = __builtin_amdgcn_exp2f(sc - m_run);
     const float p = K_::to_f(K_::from_f(pr));
-    osum[0] += p;
-    if constexpr (VSUM) lsum[0] += 0.5f * p;   // both half-waves add it: the swap below doubles it
+    if constexpr (!VSUM) osum[0] += p;
+    else lsum[0] += 0.5f * p;   // both half-waves add it: the swap below doubles it
     #pragma unroll
     for (int db = 0; db < 2; ++db)
       #pragma unroll
@@ -271,34 +264,61 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       }
   };
 
-  // tile t lives in stage t & 1.  Top of step t: tile t's DMA was issued one step
-  // earlier (own pieces: vmcnt(0); everyone's: the barrier, which also certifies
-  // that every wave finished tile t-1, whose stage now receives tile t+1).
+  // All keys for this workgroup's queries.  Tile t lives in stage t & 1.  Top of step t:
+  // tile t's DMA was issued one step earlier (own pieces: vmcnt(0); everyone's: the
+  // barrier, which also certifies that every wave finished tile t-1, whose stage now
+  // receives tile t+1).
   const int ntiles = (seq + KT - 1) / KT, nfull = seq / KT, rem = seq - nfull * KT;
   const bool valu_tail = rem > 0 && rem <= TAIL_VALU;
   const int nmma = valu_tail ? nfull : ntiles;     // tiles that go through the MFMAs
-  if (nmma > 0) issue(0, 0);
-  for (int t = 0; t < nfull; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if (t + 1 < nmma) issue((t + 1) * KT, (t + 1) & 1);
-    do_tile(t, std::false_type{});
+  auto run = [&](bool exact) __attribute__((always_inline)) {
+    #pragma unroll
+    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; osum[i] = 0.f; }
+    lsum = f32x2_t{0.f, 0.f};
+    m_run = -INFINITY;
+    if (nmma > 0) issue(0, 0);
+    if (nfull > 0) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (1 < nmma) issue(KT, 1);
+      do_tile(0, std::false_type{}, true, exact);
+    }
+    for (int t = 1; t < nfull; ++t) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (t + 1 < nmma) issue((t + 1) * KT, (t + 1) & 1);
+      do_tile(t, std::false_type{}, false, exact);
+    }
+    if (nfull < nmma) {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      do_tile(nfull, std::true_type{}, nfull == 0, exact);
+    }
+    if (valu_tail && active) {
+      for (int kk = 0; kk < rem; ++kk) tail_key(nfull * KT + kk);
+    }
+  };
+  auto row_sum = [&]() __attribute__((always_inline)) {
+    if constexpr (VSUM) {
+      const float l = lsum[0] + lsum[1];
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+      return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    } else {
+      return osum[0];
+    }
+  };
+  run(!LAZY);
+  if constexpr (LAZY) {
+    // a key far above the first half tile's max overflowed P, O or the row sum: all waves
+    // of the workgroup take the exact path over their keys again (K/V restaged; rare)
+    float chk = row_sum();
+    #pragma unroll
+    for (int i = 0; i < 16; ++i) chk += o[0][i] + o[1][i];
+    if (__builtin_amdgcn_ballot_w64(active && !__builtin_isfinite(chk))) redo = 1;
+    __syncthreads();
+    if (redo) run(true);
   }
-  if (nfull < nmma) {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    do_tile(nfull, std::true_type{});
-  }
-  if (valu_tail && active) {
-    for (int kk = 0; kk < rem; ++kk) tail_key(nfull * KT + kk);
-  }
+  const float rowsum = row_sum();
   __syncthreads();
   // ---- normalise and store: stage the wave's 32 x 64 output through LDS so each
   // query row leaves as whole 128-B lines
-  float rowsum = osum[0];
-  if constexpr (VSUM) {
-    const float l = lsum[0] + lsum[1];
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
-    rowsum = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-  }
   const float inv = 1.f / rowsum;
   u16* stg = (u16*)&smem[0][0] + wave * 32 * KS;   // 32 rows x KS (padded) per wave (18 KiB of 32)
   #pragma unroll
@@ -334,14 +354,23 @@ extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t s
   const int nq = (seq + QB - 1) / QB;
   if ((long long)nq * heads * batch > 0x7fffffffLL) return DP_ERR_SHAPE;
   dim3 grid(nq * heads * batch);
-  const float sl2 = scale * 1.4426950408889634f;
+  // softmax(s * scale) = 2^(s * scale * log2 e) / sum: sl2 is the scale in log2 units
+  const float sl2 = (float)((double)scale * 1.4426950408889634);
   hipStream_t s = (hipStream_t)stream;
-  // row sums on the VALU (35 x 577: 81.2 -> 76.5 us); DP_ATTN_VSUM=0 selects the ones-MFMA row sums
+  // A/B switches: DP_ATTN_LAZY=0 takes the max of every half tile (the exact path);
+  // DP_ATTN_VSUM=0 takes the row sums on the matrix core
+  static const bool lazy = [] { const char* e = getenv("DP_ATTN_LAZY"); return !(e && e[0] == '0'); }();
   static const bool vsum = [] { const char* e = getenv("DP_ATTN_VSUM"); return !(e && e[0] == '0'); }();
   if (dtype != DP_BF16 && dtype != DP_F16) return DP_ERR_DTYPE;
-#define DP_ATTN(K, V) hipLaunchKernelGGL((attn_kernel<K, V>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2)
-  if (dtype == DP_BF16) { if (vsum) DP_ATTN(KBF16, true); else DP_ATTN(KBF16, false); }
-  else { if (vsum) DP_ATTN(KF16, true); else DP_ATTN(KF16, false); }
+#define DP_ATTN(K, L, V) hipLaunchKernelGGL((attn_kernel<K, L, V>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2)
+#define DP_ATTN_K(K)                                                               \
+  do {                                                                             \
+    if (lazy) { if (vsum) DP_ATTN(K, true, true); else DP_ATTN(K, true, false); }  \
+    else { if (vsum) DP_ATTN(K, false, true); else DP_ATTN(K, false, false); }     \
+  } while (0)
+  if (dtype == DP_BF16) DP_ATTN_K(KBF16);
+  else DP_ATTN_K(KF16);
+#undef DP_ATTN_K
 #undef DP_ATTN
   DP_CHECK_LAUNCH();
   return 0;

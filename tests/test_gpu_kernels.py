@@ -140,23 +140,27 @@ def test_head_conv_with_fused_1x1(cuda, dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("batch,seq,spike", [(2, 577, False), (1, 100, False), (3, 64, False), (1, 1, False),
-                                             (2, 66, False), (1, 2, False), (1, 67, False),
-                                             (2, 577, True), (1, 130, True)])
+@pytest.mark.parametrize("batch,seq,spike", [(2, 577, None), (1, 100, None), (3, 64, None), (1, 1, None),
+                                             (2, 66, None), (1, 2, None), (1, 67, None),
+                                             (2, 577, "tail"), (1, 130, "tail"), (2, 577, "mid"),
+                                             (1, 100, "mid")])
 def test_attention(cuda, dt, batch, seq, spike):
     """seq 577 / 66 / 2 / 130 end in 1-2 leftover keys (the VALU tail), 100 / 67 in a partial
-    MFMA tile.  spike: the LAST key of every sequence is the scaled query of token 0, so that
-    query's running max jumps inside the tail -- the rescale branch there is exercised."""
+    MFMA tile.  spike "tail": the LAST key of every sequence is the scaled query of token 0, so
+    that query's running max jumps inside the tail -- the rescale branch there is exercised;
+    "mid": key 70 (second key tile) is 40x that query, far above the max the first half key
+    tile set: P overflows and the workgroup redoes its keys on the exact-max path."""
     g = torch.Generator().manual_seed(seq)
     H, hd = 16, 64
     qkv = rnd(batch * seq, 3 * H * hd, dt=dt, dev=cuda, gen=g, scale=2.0)
     if spike:
         x = qkv.view(batch, seq, 3, H, hd)
-        x[:, seq - 1, 1] = (x[:, 0, 0].float() * 4.0).to(dt)
-    out = torch.empty(batch * seq, H * hd, dtype=dt, device=cuda)
-    ops.attention(qkv, out, batch, seq, H, hd)
+        key, f = (seq - 1, 4.0) if spike == "tail" else (70, 40.0)
+        x[:, key, 1] = (x[:, 0, 0].float() * f).to(dt)
     q, k, v = qkv.float().reshape(batch, seq, 3, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
     ref = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(batch * seq, H * hd)
+    out = torch.empty(batch * seq, H * hd, dtype=dt, device=cuda)
+    ops.attention(qkv, out, batch, seq, H, hd)
     close(out, ref, dt, "attention")
 
 
