@@ -139,7 +139,9 @@ int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
  * (bounded spin; the output of that launch is then wrong).  It is sticky: nothing
  * but the caller clears it, so one read after a whole forward / graph replay covers
  * every launch in it.  After a timeout the flags may be left set: zero the first 1 KiB
- * (or the whole workspace) before reusing it.
+ * (or the whole workspace) before reusing it.  Bytes [2048, 3200) hold the tile-ticket
+ * queues of the persistent data-parallel engine (8 per-XCD counters + an exit counter,
+ * reset to zero by the last workgroup of each launch).
  */
 #define DP_GEMM_WS_ERROR_OFFSET 4092
 int64_t dp_gemm_workspace_size(void);

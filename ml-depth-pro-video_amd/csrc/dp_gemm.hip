@@ -60,6 +60,7 @@ struct GemmP {
   int tiles_n, tiles_m;
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
   unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
+  unsigned* tq;      // persistent engine: tile-ticket queues in the workspace (NULL: static tile walk)
 };
 
 // Process-wide ablation / fault-injection bits, set only by dp_gemm_debug_flags (tools and
@@ -922,6 +923,35 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
 // Store modes: rows (incl. row-group remap), no fused head.
 // ROWLD: the epilogue reads per-row operands (residuals, pos, the fp32 C being accumulated
 // into); without them it needs fewer VGPRs (the 320 x 256 tile is at the 256 limit).
+//
+// Dynamic tile queues (p.tq != NULL, K >= 3 steps): instead of the static walk wgid,
+// wgid + G, ... every workgroup draws its tiles from the queue of the XCD it runs on
+// (8 agent-scope ticket counters).  Queue x hands out, round by round, the tile
+// positions [x*G/8, (x+1)*G/8) of each round of G tiles -- the same XCD-contiguous
+// placement as the static walk -- and a workgroup whose own queue is empty takes from
+// the next XCD's.  A workgroup that starts late (its CU still held by a side-stream
+// kernel) therefore just takes fewer tiles instead of ending the launch on a tail.
+// The ticket for the next tile is drawn at K step 0 of the current one and read back at
+// step 1 (its latency hides under the K loop), published through an LDS word.  The
+// last workgroup to finish resets the counters (graph-replay safe, no memset).
+constexpr int TQ_BYTE_OFF = 2048;   // workspace byte offset: 8 queues + exit counter, 128 B apart
+constexpr int TQ_STRIDE = 32;       // uint32 words between counters
+__device__ __forceinline__ int tq_map(int G, int T, int x, unsigned k) {
+  const int c0 = x * G / 8, len = (x + 1) * G / 8 - c0;
+  if (len <= 0) return -1;
+  const long long t = (long long)(k / (unsigned)len) * G + c0 + (int)(k % (unsigned)len);
+  return t < T ? (int)t : -1;
+}
+// thread-0 only: tickets from queue home+q, home+q+1, ... until a valid tile or all 8 are empty
+__device__ __forceinline__ int tq_draw(unsigned* tq, int G, int T, int home, int& q) {
+  for (; q < 8; ++q) {
+    const int x = (home + q) & 7;
+    const unsigned k = __hip_atomic_fetch_add(tq + TQ_STRIDE * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t = tq_map(G, T, x, k);
+    if (t >= 0) return t;
+  }
+  return -1;
+}
 template <typename K_, int BM, int BN, bool CONV, bool RELU, bool ROWLD>
 __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
   constexpr int BKT = 64, WN = 4, WM = 2;
@@ -935,21 +965,53 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
   constexpr int CPR = TN / 8, RPI = 64 / CPR, NIT = PR / RPI;
   constexpr int STORES = (FM * 16 / PR) * NIT;                   // 16-B stores per lane per tile (16-bit C)
   static_assert(8 * PR * SROW * 4 <= STAGE && FM % (PR / 16) == 0 && NIT % 2 == 0, "staging");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  // ONE LDS array (ring + the tile-ticket word): a second __shared__ object can make hipcc
+  // put a vmcnt(0) in front of the loop's ds_reads
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 16];
+  int* const tslot = (int*)(smem + 2 * STAGE);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const int wm = wave / WN, wn = wave % WN;
   const int G = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int T = p.tiles_m * p.tiles_n;
-  if (wgid >= T) return;
-  // this workgroup's tiles are wgid, wgid + G, ...: at any moment the workgroups of one XCD
-  // (consecutive wgids) work on consecutive tiles of the band raster, as the rounds of the
-  // data-parallel launch do (shared A / B panels in that XCD's L2)
-  const int t_begin = wgid;
+  const bool dyn = p.tq != nullptr;
+  int t_begin;
+  int home = 0, tq_q = 0;      // thread 0: home queue, queues found empty so far
+  unsigned tq_k = 0;           // thread 0: ticket drawn at K step 0
+  if (dyn) {
+    if (tid == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      home = (int)(xcc & 7);
+      tslot[0] = tq_draw(p.tq, G, T, home, tq_q);
+    }
+    lds_barrier();
+    t_begin = __builtin_amdgcn_readfirstlane(tslot[0]);
+  } else {
+    // static walk: this workgroup's tiles are wgid, wgid + G, ...: at any moment the
+    // workgroups of one XCD (consecutive wgids) work on consecutive tiles of the band
+    // raster, as the rounds of the data-parallel launch do (shared A / B panels in that
+    // XCD's L2)
+    const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    t_begin = wgid < T ? wgid : -1;
+  }
+  // every workgroup counts itself out; the last one resets the queues for the next launch
+  auto leave = [&]() {
+    if (dyn && tid == 0) {
+      const unsigned d = __hip_atomic_fetch_add(p.tq + TQ_STRIDE * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (unsigned)G - 1u) {
+        #pragma unroll
+        for (int x = 0; x <= 8; ++x) __hip_atomic_store(p.tq + TQ_STRIDE * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  if (t_begin < 0) {
+    leave();
+    return;
+  }
 
   const int prow = wave * 8 + (lane >> 3);
   const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
@@ -1036,27 +1098,48 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
   setup(m0, n0);
   issue(0, 0);
   int stage = 0;
-  for (int t = t_begin;; ) {
+  for (int t = t_begin, first = 1;; first = 0) {
     #pragma unroll
     for (int i = 0; i < FM; ++i)
       #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const bool has_next = t + G < T;
+    int t_next = t + G < T ? t + G : -1;
     int m0n = 0, n0n = 0;
     for (int kt = 0; kt < KT; ++kt) {
       // step 0 of a later tile: only its own DMA (issued before the previous epilogue's
       // STORES stores) has to have landed; the stores may still be draining
-      if (kt == 0 && t != t_begin) wait_vmcnt<STORES>();
+      if (kt == 0 && !first) wait_vmcnt<STORES>();
       else wait_vmcnt<0>();
       lds_barrier();
+      if (dyn && tid == 0) {
+        // next tile's ticket: drawn at step 0, resolved at step 1 (after its vmcnt(0)),
+        // read by every wave at step KT-1 >= 2, behind a barrier
+        if (kt == 0 && tq_q < 8)
+          tq_k = __hip_atomic_fetch_add(p.tq + TQ_STRIDE * ((home + tq_q) & 7), 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        if (kt == 1) {
+          int tn_ = -1;
+          if (tq_q < 8) {
+            tn_ = tq_map(G, T, (home + tq_q) & 7, tq_k);
+            if (tn_ < 0) {
+              ++tq_q;
+              tn_ = tq_draw(p.tq, G, T, home, tq_q);
+            }
+          }
+          tslot[0] = tn_;
+        }
+      }
       if (kt + 1 < KT) {
         issue(kt + 1, stage ^ 1);
-      } else if (has_next) {
-        tile_coords(p, t + G, tm, tn);
-        m0n = tm * BM;
-        n0n = tn * BN;
-        setup(m0n, n0n);
-        issue(0, stage ^ 1);
+      } else {
+        if (dyn) t_next = __builtin_amdgcn_readfirstlane(tslot[0]);
+        if (t_next >= 0) {
+          tile_coords(p, t_next, tm, tn);
+          m0n = tm * BM;
+          n0n = tn * BN;
+          setup(m0n, n0n);
+          issue(0, stage ^ 1);
+        }
       }
       compute(stage);
       stage ^= 1;
@@ -1098,11 +1181,12 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
       // the next pass rewrites this wave's slab: its reads of this pass are done first
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    if (!has_next) break;
-    t += G;
+    if (t_next < 0) break;
+    t = t_next;
     m0 = m0n;
     n0 = n0n;
   }
+  leave();
 }
 
 // ======================================================= 8-phase 256x256 engine
@@ -1915,6 +1999,10 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       // in-frame (199-203 us both, profiles/r01s_fc1_engine_ab/)
       else if (cost320 < cost256) tile = DP_TILE_BIG_320x256;
       else tile = (tiles256 >= 600 && a->a_mode != DP_A_CONV) ? DP_TILE_8PH_256x256 : DP_TILE_BIG_256x256;
+      // A/B switches for the fc1 shape (8-phase by default): debug 8192 -> 320 x 256,
+      // 16384 -> 256 x 256 (both persistent below when eligible)
+      if (tile == DP_TILE_8PH_256x256 && (dbg & 8192)) tile = DP_TILE_BIG_320x256;
+      else if (tile == DP_TILE_8PH_256x256 && (dbg & 16384)) tile = DP_TILE_BIG_256x256;
     }
   }
   // byte extent of C for the persistent engine's bounded buffer stores (0: not eligible)
@@ -1937,7 +2025,14 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     // dense (ViT) GEMMs only with debug 2048: they run beside the side encoders, and a
     // persistent grid whose workgroups cannot all start at once ends on a tail (qkv: 146 ->
     // 140 us alone, frame 23.74 -> 23.89 ms in-frame)
-    const bool dense_ok = a->a_mode == DP_A_CONV || (dbg & 2048);
+    // debug 4096: persistent grids draw their tiles from per-XCD queues (a late workgroup
+    // takes fewer tiles), dense GEMMs included.  Measured and rejected (round 2, same box,
+    // graph replay, 2 x 4 runs): 42.55 / 42.65 fps off; queues + persistent qkv 42.27 /
+    // 42.13; + fc1 on the persistent 320 x 256 42.0 / 42.0, on 256 x 256 41.9 / 41.95.  Eager
+    // serial: qkv 136.5 (data-parallel 320 x 256) vs 139.4 us, fc1 195.8 (8-phase) vs 196.4
+    // / 199.8 us, 768^2 conv 711 vs 712 us (profiles/r02i_tile_queues/).
+    const bool dyn_ok = ws_ok && a->K / 64 >= 3 && (dbg & 4096);
+    const bool dense_ok = a->a_mode == DP_A_CONV || (dbg & 2048) || dyn_ok;
     if (dense_ok && tile == DP_TILE_BIG_320x256 && (long long)((a->M + 319) / 320) * (a->N / 256) >= 2 * ncu)
       tile = DP_TILE_PBIG_320x256;
     else if (dense_ok && tile == DP_TILE_BIG_256x256 && tiles256 >= 2 * ncu)
@@ -1966,6 +2061,12 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   p.dbg = dbg;
   p.c_bytes = c_bytes;
+  p.tq = nullptr;
+  // persistent launches with a workspace and >= 3 K steps take their tiles from the queues:
+  // debug 4096 (measured slower, above), or an explicit PBIG tile hint with a workspace
+  if ((tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) && ws_ok && a->K / 64 >= 3 &&
+      ((dbg & 4096) || a->tile != DP_TILE_AUTO))
+    p.tq = (unsigned*)((char*)a->workspace + TQ_BYTE_OFF);
   return 0;
 }
 }  // namespace

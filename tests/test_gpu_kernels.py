@@ -459,3 +459,71 @@ def test_persistent_engine_bit_identical_to_data_parallel(cuda, dt, pair, case):
     ops.gemm(A, B, C2, M=M, N=N, K=K, tile=tb, **kw)
     torch.cuda.synchronize()
     assert torch.equal(C1, C2), (C1.float() - C2.float()).abs().max().item()
+
+
+@pytest.mark.parametrize("pair", ["320", "256"])
+@pytest.mark.parametrize("case", ["dense_bias", "gelu_ragged", "acc_f32"])
+def test_persistent_engine_tile_queues(cuda, pair, case):
+    """With a workspace the persistent engine draws its tiles from the per-XCD ticket queues
+    (dp_gemm.hip tq_draw): bit-identical to the data-parallel engine, every counter back at
+    zero after each launch (last workgroup resets them), also for back-to-back launches,
+    under HIP-graph replay, and beside a concurrent GEMM on another stream that holds CUs
+    while the persistent grid starts (late workgroups take fewer tiles)."""
+    from depth_pro._lib import DP_TILE_PBIG_256x256, DP_TILE_PBIG_320x256
+
+    dt = torch.bfloat16
+    tp, tb = (DP_TILE_PBIG_320x256, DP_TILE_BIG_320x256) if pair == "320" else (DP_TILE_PBIG_256x256,
+                                                                                  DP_TILE_BIG_256x256)
+    g = torch.Generator().manual_seed(11 + sum(map(ord, case)))
+    M, N, K = {"dense_bias": (20195, 3072, 1024), "gelu_ragged": (4999, 1536, 512),
+               "acc_f32": (3001, 1024, 2048)}[case]
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    kw = dict(bias=torch.randn(N, generator=g).to(cuda))
+    if case == "gelu_ragged":
+        kw.update(act=DP_ACT_GELU)
+    if case == "acc_f32":
+        kw.update(gamma=torch.rand(N, generator=g).to(cuda), accumulate=True)
+        C0 = torch.randn(M, N, generator=g).to(cuda)
+    else:
+        C0 = torch.full((M, N), 7.0, dtype=dt, device=cuda)
+    ws = ops.gemm_workspace(cuda)
+    q = ws[2048:3200].view(torch.int32)
+    ref = C0.clone()
+    ops.gemm(A, B, ref, M=M, N=N, K=K, tile=tb, **kw)
+    for _ in range(3):                                  # back to back: counters reset in between
+        C = C0.clone()
+        ops.gemm(A, B, C, M=M, N=N, K=K, tile=tp, workspace=ws, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(C, ref), (C.float() - ref.float()).abs().max().item()
+        assert int(q.abs().sum()) == 0, q.nonzero()
+    # beside a long GEMM on another stream (its own workspace)
+    side = torch.cuda.Stream(device=cuda)
+    ws2 = ops.gemm_workspace(cuda)
+    A2 = rnd(8192, 4096, dt=dt, dev=cuda, gen=g)
+    B2 = rnd(4096, 4096, dt=dt, dev=cuda, gen=g, scale=4096 ** -0.5)
+    C2 = torch.empty(8192, 4096, dtype=dt, device=cuda)
+    C = C0.clone()
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(side):
+        ops.gemm(A2, B2, C2, M=8192, N=4096, K=4096, workspace=ws2)
+    ops.gemm(A, B, C, M=M, N=N, K=K, tile=tp, workspace=ws, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C, ref)
+    assert int(q.abs().sum()) == 0
+    # graph replay
+    C = C0.clone()
+    gr = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(gr, stream=s):
+            ops.gemm(A, B, C, M=M, N=N, K=K, tile=tp, workspace=ws, **kw)
+    torch.cuda.current_stream(cuda).wait_stream(s)
+    for _ in range(2):
+        if case == "acc_f32":
+            C.copy_(C0)
+        gr.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(C, ref)
+        assert int(q.abs().sum()) == 0
