@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 4
+#define DP_ABI_VERSION 5
 int dp_abi_version(void);
 
 /*
@@ -140,8 +140,9 @@ int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
  * but the caller clears it, so one read after a whole forward / graph replay covers
  * every launch in it.  After a timeout the flags may be left set: zero the first 1 KiB
  * (or the whole workspace) before reusing it.  Bytes [2048, 3200) hold the tile-ticket
- * queues of the persistent data-parallel engine (8 per-XCD counters + an exit counter,
- * reset to zero by the last workgroup of each launch).
+ * queues of the persistent data-parallel engine (8 per-XCD counters + an exit counter),
+ * bytes [3200, 4088) the row-band counters of dp_gemm_ln's fused LayerNorm: both reset
+ * to zero by the last workgroup that uses them in each launch.
  */
 #define DP_GEMM_WS_ERROR_OFFSET 4092
 int64_t dp_gemm_workspace_size(void);
@@ -152,6 +153,26 @@ int64_t dp_gemm_workspace_size(void);
  * persistent engine), *grid the workgroup count.  For tests and the bench.
  */
 int dp_gemm_plan(const dp_gemm_args* args, int32_t* tile, int32_t* grid);
+
+/*
+ * dp_gemm_ln: dp_gemm, then y[r] = LN(C[r, 0:N]) * w + b (eps, two-pass-exact mean /
+ * variance in fp32) written as `ln_dtype` rows of stride ld_ln -- the residual-stream
+ * update of a timm Block followed by the NEXT LayerNorm (norm2 after attn.proj, the next
+ * block's norm1 or the final norm after mlp.fc2: vision_transformer.py Block.forward,
+ * reference network/vit_factory.py:68-124).  Requires DP_STORE_ROWS without a row-group
+ * remap and an fp32 C.  When the launch fits one round of workgroups on the dense
+ * 320x256 / 256x128 engines and `args->workspace` is set, the LayerNorm runs in the GEMM's
+ * epilogue: each workgroup publishes per-row (mean, M2) partials of its columns, the
+ * workgroups of a row band meet through counters in the workspace (bounded wait: a
+ * timeout sets the sticky error word), and every workgroup normalises the rows it holds
+ * in registers -- no fp32 re-read of C.  Otherwise the GEMM and a dp_layernorm pass run
+ * back to back (same result up to fp32 summation order).  Because fused workgroups wait
+ * for the rest of their band, never run two fused launches (or a fused launch and a
+ * stream-K launch) concurrently on one device: each could hold the CUs the other's
+ * undispatched workgroups need.  Beside kernels that do not wait it is safe.
+ */
+int dp_gemm_ln(const dp_gemm_args* args, const float* ln_w, const float* ln_b, void* ln_out, int64_t ld_ln,
+               float eps, int32_t ln_dtype, dp_stream_t stream);
 
 /*
  * dp_layernorm: y[r] = LN(x[r]) * w + b over `cols`, fp32 in, 16-bit out.

@@ -61,6 +61,16 @@ struct GemmP {
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
   unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
   unsigned* tq;      // persistent engine: tile-ticket queues in the workspace (NULL: static tile walk)
+  // fused LayerNorm of the rows of C (dp_gemm_ln): gemm_big_kernel<..., LNF = true> only
+  const float* ln_w;
+  const float* ln_b;
+  u16* ln_out;
+  long long ld_ln;
+  float ln_eps;
+  int ln_f16;        // LN output kind: 1 f16, 0 bf16
+  unsigned long long* ln_part;  // [N / TN][M] (mean, M2) pairs of every wave's TN columns
+  unsigned* ln_cnt;  // per row band: arrivals, departures
+  unsigned* err;     // sticky workspace error word
 };
 
 // Process-wide ablation / fault-injection bits, set only by dp_gemm_debug_flags (tools and
@@ -619,7 +629,7 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
   }
 }
 
-template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU>
+template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, bool LNF = false>
 __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   // 8 waves as WM x WN; the 512 x 128 tile (N = 128 layers) uses 4 x 2 so that every
   // wave still owns a 128 x 64 sub-tile (same fragment reuse as the 256 x 256 tile)
@@ -897,13 +907,129 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
         for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
         ms[it] = m0 + wm * TM + q * 32 + row;
       }
-      if constexpr (TN % 32 == 0) {
+      if constexpr (TN % 32 == 0 && !LNF) {
         if (p.store_mode == DP_STORE_HEAD_PS) {
           head_ps_rows<NITC>(p, cc, ms, n_l, v, lane);
           continue;
         }
       }
       epilogue_rows<K_, NITC>(p, cc, ms, n_l, v);
+      if constexpr (LNF) {
+        // the new rows stay in the registers of the accumulators this pass consumed
+        // (8 * FN floats per lane per pass, same count), and each wave publishes, per row,
+        // the mean and centred sum of squares of its TN columns (Chan's pairwise form)
+        #pragma unroll
+        for (int it = 0; it < NITC; ++it) {
+          float sm = 0.f;
+          #pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int idx = (c0 + it) * 8 + r;
+            acc[2 * q + idx / (4 * FN)][(idx % (4 * FN)) / 4][idx % 4] = v[it][r];
+            sm += v[it][r];
+          }
+          #pragma unroll
+          for (int o = 1; o < CPR; o <<= 1) sm += __shfl_xor(sm, o);
+          const float mw = sm * (1.f / TN);
+          float m2 = 0.f;
+          #pragma unroll
+          for (int r = 0; r < 8; ++r) m2 += (v[it][r] - mw) * (v[it][r] - mw);
+          #pragma unroll
+          for (int o = 1; o < CPR; o <<= 1) m2 += __shfl_xor(m2, o);
+          if (lane % CPR == 0 && ms[it] < p.M) {
+            const unsigned long long pk = (unsigned long long)__float_as_uint(mw) |
+                                          ((unsigned long long)__float_as_uint(m2) << 32);
+            __hip_atomic_store(p.ln_part + (long long)(tile_n * WN + wn) * p.M + ms[it], pk, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);   // write-through: read by other XCDs
+          }
+        }
+      }
+    }
+  }
+  if constexpr (LNF) {
+    // Band hand-off (the tiles_n workgroups of this row band, all resident: the host only
+    // fuses single-round grids): publish -- every wave's partial stores done, then ONE
+    // agent-scope arrival add -- and wait for the band's other arrivals (bounded spin:
+    // a timeout sets the sticky error word and the LN rows of this band are wrong).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* const arr = p.ln_cnt + 2 * tile_m;
+    if (tid == 0) {
+      __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned n = 0;
+      while (__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)p.tiles_n) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n == (1u << 22)) {
+          __hip_atomic_fetch_or(p.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    // per row: mean and M2 of all N / TN partials (each lane of the row's CPR lanes combines
+    // every CPR-th partial), then (x - mean) * rstd * w + b -> 16-bit, 16-B stores
+    const int P = p.N / TN, c_ = lane % CPR;
+    float lw[8], lb[8];
+    {
+      const int nc = n_l < p.N ? n_l : p.N - 8;
+      const float4 w0 = *(const float4*)(p.ln_w + nc), w1 = *(const float4*)(p.ln_w + nc + 4);
+      const float4 b0 = *(const float4*)(p.ln_b + nc), b1 = *(const float4*)(p.ln_b + nc + 4);
+      lw[0] = w0.x; lw[1] = w0.y; lw[2] = w0.z; lw[3] = w0.w; lw[4] = w1.x; lw[5] = w1.y; lw[6] = w1.z; lw[7] = w1.w;
+      lb[0] = b0.x; lb[1] = b0.y; lb[2] = b0.z; lb[3] = b0.w; lb[4] = b1.x; lb[5] = b1.y; lb[6] = b1.z; lb[7] = b1.w;
+    }
+    const float inv_n = 1.f / (float)p.N;
+    #pragma unroll
+    for (int q = 0; q < FM / 2; ++q) {
+      #pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int m = m0 + wm * TM + q * 32 + it * RPI + lane / CPR;
+        const int mc = m < p.M ? m : p.M - 1;
+        float smean = 0.f, ssq = 0.f, ms_[8], m2_[8];
+        int np = 0;
+        #pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int j = c_ + k * CPR;
+          if (j < P) {
+            const unsigned long long pk =
+                __hip_atomic_load(p.ln_part + (long long)j * p.M + mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ms_[k] = __uint_as_float((unsigned)pk);
+            m2_[k] = __uint_as_float((unsigned)(pk >> 32));
+            smean += ms_[k];
+            ++np;
+          }
+        }
+        #pragma unroll
+        for (int o = 1; o < CPR; o <<= 1) smean += __shfl_xor(smean, o);
+        const float mean = smean / (float)P;
+        #pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k < np) ssq += m2_[k] + (float)TN * (ms_[k] - mean) * (ms_[k] - mean);
+        #pragma unroll
+        for (int o = 1; o < CPR; o <<= 1) ssq += __shfl_xor(ssq, o);
+        const float rstd = rsqrtf(ssq * inv_n + p.ln_eps);
+        float h[8];
+        #pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int idx = it * 8 + r;
+          h[r] = (acc[2 * q + idx / (4 * FN)][(idx % (4 * FN)) / 4][idx % 4] - mean) * rstd * lw[r] + lb[r];
+        }
+        uint4 o;
+        if (p.ln_f16) {
+          o.x = KF16::pack2(h[0], h[1]); o.y = KF16::pack2(h[2], h[3]);
+          o.z = KF16::pack2(h[4], h[5]); o.w = KF16::pack2(h[6], h[7]);
+        } else {
+          o.x = KBF16::pack2(h[0], h[1]); o.y = KBF16::pack2(h[2], h[3]);
+          o.z = KBF16::pack2(h[4], h[5]); o.w = KBF16::pack2(h[6], h[7]);
+        }
+        if (m < p.M && n_l < p.N) *(uint4*)(p.ln_out + (long long)m * p.ld_ln + n_l) = o;
+      }
+    }
+    // departures: the band's last workgroup out resets both counters for the next launch
+    if (tid == 0) {
+      const unsigned d = __hip_atomic_fetch_add(arr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (unsigned)p.tiles_n - 1u) {
+        __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(arr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   DP_STAMP(st3_);
@@ -1840,6 +1966,18 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_m = (p.M + BM - 1) / BM;
   dim3 grid(p.tiles_n * p.tiles_m);
+  // fused LayerNorm epilogue (dp_gemm_ln): only the dense residual-accumulate engines of the
+  // ViT proj / fc2 GEMMs have an LNF instantiation; dp_gemm_ln checks eligibility first
+  if (p.ln_out) {
+    if constexpr (BKT == 64 && ((BM == 320 && BN == 256 && !PIPE) || (BM == 256 && BN == 128 && PIPE))) {
+      if (conv || p.relu_a) return DP_ERR_ARG;
+      hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, false, true>), grid, dim3(NT_BIG), 0, s,
+                         p);
+      DP_CHECK_LAUNCH();
+      return 0;
+    }
+    return DP_ERR_ARG;
+  }
   if (conv && p.relu_a)
     hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, true, true>), grid, dim3(NT_BIG), 0, s, p);
   else if (conv)
@@ -2062,6 +2200,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.dbg = dbg;
   p.c_bytes = c_bytes;
   p.tq = nullptr;
+  p.ln_w = p.ln_b = nullptr; p.ln_out = nullptr; p.ld_ln = 0; p.ln_eps = 0.f; p.ln_f16 = 0;
+  p.ln_part = nullptr; p.ln_cnt = nullptr; p.err = nullptr;
   // persistent launches with a workspace and >= 3 K steps take their tiles from the queues:
   // debug 4096 (measured slower, above), or an explicit PBIG tile hint with a workspace
   if ((tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) && ws_ok && a->K / 64 >= 3 &&
@@ -2093,6 +2233,47 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
   if (tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) grid = grid < num_cus() ? grid : num_cus();
   if (grid_out) *grid_out = tile == DP_TILE_STREAMK_256x256 ? sk_grid(p) : grid;
   return 0;
+}
+
+// byte offset of the fused-LN band counters in the workspace (after the tile queues, before
+// the error word): 2 words per row band
+constexpr int LN_CNT_OFF = 3200, LN_MAX_BANDS = (DP_GEMM_WS_ERROR_OFFSET - LN_CNT_OFF) / 8;
+
+extern "C" int dp_gemm_ln(const dp_gemm_args* a, const float* ln_w, const float* ln_b, void* ln_out, int64_t ld_ln,
+                          float eps, int32_t ln_dtype, dp_stream_t stream) {
+  if (!a || !ln_w || !ln_b || !ln_out) return DP_ERR_ARG;
+  if (ln_dtype != DP_BF16 && ln_dtype != DP_F16) return DP_ERR_DTYPE;
+  if (a->store_mode != DP_STORE_ROWS || a->row_group || a->c_dtype != DP_F32 || a->head_w || ld_ln < a->N ||
+      ld_ln % 8 != 0 || ((uintptr_t)ln_out & 15))
+    return DP_ERR_ARG;
+  GemmP p;
+  int tile = 0;
+  int rc = gemm_plan(a, p, tile);
+  if (rc) return rc;
+  const int bm = tile == DP_TILE_BIG_320x256 ? 320 : 256, bn = tile == DP_TILE_BIG_320x256 ? 256 : 128;
+  const long long tm = (a->M + bm - 1) / bm, tn = a->N / bn;
+  const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
+  // fused: one of the two LNF engines, a single round of workgroups (every workgroup of a row
+  // band resident at once, so the band hand-off cannot wait on an undispatched one), N a
+  // whole number of tiles (every column's partial written)
+  const bool fuse = (tile == DP_TILE_BIG_320x256 || tile == DP_TILE_BIG_256x128) && a->a_mode == DP_A_DENSE &&
+                    !a->relu_a && ws_ok && a->N % bn == 0 && tm * tn <= num_cus() && tm <= LN_MAX_BANDS &&
+                    (long long)a->N / (bn / 4) * a->M * 8 <= a->workspace_bytes - SK_FLAG_BYTES &&
+                    !(p.dbg & 65536);
+  hipStream_t s = (hipStream_t)stream;
+  if (!fuse) {   // unfused: the GEMM, then the LayerNorm pass over C
+    rc = dp_gemm(a, stream);
+    if (rc) return rc;
+    return dp_layernorm((const float*)a->C, a->ldc, ln_w, ln_b, ln_out, ld_ln, a->M, a->N, eps, ln_dtype, stream);
+  }
+  char* ws = (char*)a->workspace;
+  p.ln_w = ln_w; p.ln_b = ln_b; p.ln_out = (u16*)ln_out; p.ld_ln = ld_ln; p.ln_eps = eps;
+  p.ln_f16 = ln_dtype == DP_F16;
+  p.ln_part = (unsigned long long*)(ws + SK_FLAG_BYTES);
+  p.ln_cnt = (unsigned*)(ws + LN_CNT_OFF);
+  p.err = (unsigned*)(ws + DP_GEMM_WS_ERROR_OFFSET);
+  if (a->dtype == DP_BF16) return launch_k<KBF16>(p, tile, false, s);
+  return launch_k<KF16>(p, tile, false, s);
 }
 
 extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {

@@ -317,11 +317,17 @@ class Engine:
         self.side_streams = int(os.environ.get("DP_SIDE_STREAMS", "2"))
         # GEMM engine of the side encoders' block GEMMs (DP_SIDE_TILE, a DP_TILE_* value; 0 = planner)
         self.side_tile = int(os.environ.get("DP_SIDE_TILE", "0"))
+        # ViT LayerNorms fused into the patch encoder's proj / fc2 epilogues (dp_gemm_ln, DP_LN_FUSE=1).
+        # Measured and rejected (round 2, profiles/r02k_ln_fuse/): 40.35 / 40.44 fps fused vs 41.84 /
+        # 41.73 separate; eager proj + LN 100.6 us fused vs 67.8 + 22.5, fc2 + LN 194.2 vs 169.8 + 22.5:
+        # the row-band wait (every workgroup waits for the slowest of its band) and the normalise
+        # pass after it cost more than the LayerNorm pass they replace.
+        self.ln_fuse = os.environ.get("DP_LN_FUSE", "0") == "1"
         if self.side_mode not in ("concurrent", "serial", "late"):
             raise DPError(f"DP_SIDE_MODE={self.side_mode!r}")
 
     # ------------------------------------------------------------------ ViT
-    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
+    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, ln_fuse=False):
         P, M = self.P, n_img * TOK
         # side encoders (one image, M = 577): engine choice for CU-time, not latency (DP_SIDE_TILE)
         t = self.side_tile if n_img == 1 else 0
@@ -330,28 +336,43 @@ class Engine:
                  A_off=cols_off_rows * 768, bias=P[pre + "pe.b"], pos=P[pre + "pos"], ldpos=D,
                  pos_group=PTOK, pos_off=1, row_group=PTOK, row_group_out=TOK, row_off=1)
         ops.vit_cls_rows(buf.x, P[pre + "cls"], P[pre + "pos"], n_img)
+        # LayerNorms fused into the residual GEMMs (dp_gemm_ln): norm2 rides on attn.proj, the
+        # next block's norm1 (or the final norm) on mlp.fc2; only block 0's norm1 -- after the
+        # patch embedding, whose cls rows come from another kernel -- is a pass of its own
+        # Its workgroups wait for the other workgroups of their row band, so two such launches
+        # must never run at once (each could hold CUs the other's missing workgroups need):
+        # only the patch encoder, alone on the main stream, uses it (ln_fuse), never the side
+        # encoders beside it nor concurrent window groups.
+        fuse = ln_fuse and self.ln_fuse and "ln" not in _ABLATE and "vitgemm" not in _ABLATE
         for i in range(DEPTH):
             b = f"{pre}blocks.{i}."
-            if "ln" not in _ABLATE:
+            if "ln" not in _ABLATE and (i == 0 or not fuse):
                 ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"],
                          tile=t)
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS)
+            ln2 = (P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, 1e-6) if fuse else None
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
-                         gamma=P[b + "ls1.gamma"], accumulate=True, tile=t)
-            if "ln" not in _ABLATE:
+                         gamma=P[b + "ls1.gamma"], accumulate=True, tile=t, ln=ln2)
+            if "ln" not in _ABLATE and not fuse:
                 ops.layernorm(buf.x, P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, M, D)
+            nb = f"{pre}blocks.{i + 1}."
+            ln1 = None
+            if fuse:
+                ln1 = ((P[nb + "norm1.weight"], P[nb + "norm1.bias"], buf.h, 1e-6) if i + 1 < DEPTH else
+                       (P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, 1e-6))
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
                          act=DP_ACT_GELU, tile=t)
                 ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
-                         gamma=P[b + "ls2.gamma"], accumulate=True, tile=t)
+                         gamma=P[b + "ls2.gamma"], accumulate=True, tile=t, ln=ln1)
             if hooks and i in hooks:
                 hooks[i]()
-        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
+        if not fuse:
+            ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
@@ -497,7 +518,7 @@ class Engine:
                 5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
                 11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
             }
-            self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks)
+            self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True)
         else:
             self._patch_groups(main)
         ops.merge_windows(vp.out, 0, 5, 3, self.f0)
@@ -604,5 +625,5 @@ class Engine:
             self._err_host.zero_()
             for w in [self.ws_main, self.ws_side, self.ws_side2] + self.ws_groups:
                 w.zero_()   # error word, and any hand-off flag the timed-out launch left set
-            raise DPError("dp_gemm stream-K: a partial-tile hand-off timed out; the depth map of a recent "
-                          "frame is invalid (workspace error word set)")
+            raise DPError("dp_gemm: a stream-K partial-tile or fused-LayerNorm row-band hand-off timed out; "
+                          "the depth map of a recent frame is invalid (workspace error word set)")

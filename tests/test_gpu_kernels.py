@@ -527,3 +527,70 @@ def test_persistent_engine_tile_queues(cuda, pair, case):
         torch.cuda.synchronize()
         assert torch.equal(C, ref)
         assert int(q.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("case", ["patch_proj", "patch_fc2", "side_fc2", "ragged", "unfused_big", "f16_out",
+                                  "forced_unfused"])
+def test_gemm_residual_layernorm(cuda, case):
+    """dp_gemm_ln: the residual-accumulate GEMM (timm Block: x += ls * (h W^T + b)) and the next
+    LayerNorm of the new rows.  C is bit-identical to dp_gemm; the LN rows match an fp32 torch
+    LayerNorm of that C to the 16-bit rounding of the output (the fused epilogue combines
+    per-wave (mean, M2) partials exactly, only the fp32 summation order differs); the row-band
+    counters are back at zero after every launch and under graph replay.  Shapes: the patch
+    encoder's proj / fc2 (M = 20195, one round of 256 workgroups on the 320x256 engine), a side
+    encoder's fc2 (M = 577, 256x128 engine), a ragged M, a grid too large to fuse (GEMM + LN
+    pass), an f16 LN output, and the unfused path forced by debug bit 65536."""
+    from depth_pro import _lib
+
+    M, K, odt = {"patch_proj": (20195, 1024, torch.bfloat16), "patch_fc2": (20195, 4096, torch.bfloat16),
+                 "side_fc2": (577, 4096, torch.bfloat16), "ragged": (3001, 2048, torch.bfloat16),
+                 "unfused_big": (40000, 1024, torch.bfloat16), "f16_out": (577, 1024, torch.float16),
+                 "forced_unfused": (20195, 1024, torch.bfloat16)}[case]
+    N, dt = 1024, torch.bfloat16
+    g = torch.Generator().manual_seed(sum(map(ord, case)))
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    kw = dict(bias=torch.randn(N, generator=g).to(cuda), gamma=torch.rand(N, generator=g).to(cuda), accumulate=True)
+    # a residual stream with a per-row offset and a few large channels (mean far from 0)
+    x0 = (torch.randn(M, N, generator=g) * 2 + torch.randn(M, 1, generator=g) * 5).to(cuda)
+    x0[:, 7] += 40.0
+    w = (1 + 0.1 * torch.randn(N, generator=g)).to(cuda)
+    b = (0.1 * torch.randn(N, generator=g)).to(cuda)
+    ws = ops.gemm_workspace(cuda)
+    cnt = ws[3200:4088].view(torch.int32)
+    ref = x0.clone()
+    ops.gemm(A, B, ref, M=M, N=N, K=K, workspace=ws, **kw)
+    lref = F.layer_norm(ref, (N,), w, b, eps=1e-6)
+    lib = _lib.load()
+    if case == "forced_unfused":
+        lib.dp_gemm_debug_flags(65536)
+    try:
+        for _ in range(2):
+            C = x0.clone()
+            y = torch.full((M, N), float("nan"), dtype=odt, device=cuda)
+            ops.gemm(A, B, C, M=M, N=N, K=K, workspace=ws, ln=(w, b, y, 1e-6), **kw)
+            torch.cuda.synchronize()
+            assert torch.equal(C, ref)
+            err = (y.float() - lref).abs()
+            tol = lref.abs() * (2.0 ** -8 if odt == torch.bfloat16 else 2.0 ** -11) + 1e-4
+            assert bool((err <= tol).all()), (err - tol).max().item()
+            assert int(cnt.abs().sum()) == 0 and ops.workspace_error(ws) == 0
+    finally:
+        lib.dp_gemm_debug_flags(0)
+    if case == "patch_fc2":   # graph replay of the fused launch
+        C = x0.clone()
+        y = torch.empty(M, N, dtype=odt, device=cuda)
+        gr = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=cuda)
+        s.wait_stream(torch.cuda.current_stream(cuda))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(gr, stream=s):
+                ops.gemm(A, B, C, M=M, N=N, K=K, workspace=ws, ln=(w, b, y, 1e-6), **kw)
+        torch.cuda.current_stream(cuda).wait_stream(s)
+        for _ in range(2):
+            C.copy_(x0)
+            gr.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(C, ref)
+            assert bool(((y.float() - lref).abs() <= lref.abs() * 2.0 ** -8 + 1e-4).all())
+            assert int(cnt.abs().sum()) == 0 and ops.workspace_error(ws) == 0

@@ -215,12 +215,15 @@ def test_config5_4k_frame_vs_reference(model, golden_dir):
 @pytest.mark.parametrize("groups", [2, 3])
 def test_patch_window_groups_match_single_group(model, groups):
     """The patch encoder run as concurrent window groups (Engine.set_patch_groups) gives the same
-    canonical inverse depth and FOV as one group: the same per-element K order everywhere."""
+    canonical inverse depth and FOV as one group: the same per-element K order everywhere.
+    (Window groups run concurrently, so they never use the fused residual LayerNorm, whose
+    row statistics are summed in another fp32 order: the single group runs unfused too.)"""
     m, transform = model
     e = m.engine()
     x = transform(frame(6))
-    n0 = len(e.patch_groups)
+    n0, f0 = len(e.patch_groups), e.ln_fuse
     try:
+        e.ln_fuse = False
         e.set_patch_groups(1)
         c1, f1 = (t.clone() for t in m.forward(x.unsqueeze(0)))
         e.set_patch_groups(groups)
@@ -230,6 +233,7 @@ def test_patch_window_groups_match_single_group(model, groups):
         print(f"\n[{m.tag}] {groups} window groups: max|d canonical| {d:.3e}")
         assert torch.equal(cg, c1) and torch.equal(fg, f1)
     finally:
+        e.ln_fuse = f0
         e.set_patch_groups(n0)
 
 
@@ -267,3 +271,25 @@ def ops_resize(x3, e):
     from depth_pro import ops
 
     ops.resize_bilinear(x3, e.x0)
+
+
+def test_forward_fused_layernorm_vs_reference(model, golden_dir):
+    """The opt-in fused residual LayerNorm path (DP_LN_FUSE=1: dp_gemm_ln in the patch
+    encoder's proj / fc2) meets the same parity bounds as the default separate passes."""
+    m, transform = model
+    e = m.engine()
+    g = np.load(f"{golden_dir}/golden_forward_frame0.npz")
+    x = transform(frame(0)).unsqueeze(0)
+    f0, graph = e.ln_fuse, e.graph
+    try:
+        e.ln_fuse, e.graph = True, None
+        with torch.no_grad():
+            canonical, fov = m.forward(x)
+        e.check_status(block=True)
+        c = canonical[0, 0, ::8, ::8].float().cpu().numpy()
+        e_c = rel_l1(c, g["canonical_sub8"])
+        e_f = abs(fov.item() - float(g["fov_deg"][0])) / abs(float(g["fov_deg"][0]))
+        print(f"\n[{m.tag}] fused LN: canonical rel-L1 {e_c:.3e}  fov rel {e_f:.2e}")
+        assert e_c < m.tol["canon"] and e_f < m.tol["fov"]
+    finally:
+        e.ln_fuse, e.graph = f0, graph
