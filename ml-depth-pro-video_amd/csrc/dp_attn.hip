@@ -66,8 +66,12 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
 // (m_run moves when exceeded by > 8, so P <= 256) -- rare on real inputs, checked once.
 // VSUM: row sums of P as f32 VALU adds (2 packed adds per 4 scores) instead of an MFMA
 // against an all-ones operand (4 MFMAs per 64-key tile).
-template <typename K_, bool LAZY, bool VSUM>
-__global__ void __launch_bounds__(256, 4)
+// PF: software-prefetched fragments -- a half tile's V^T fragments are read before its
+// softmax and the next half's K fragments before its PV MFMAs, so their LDS latency hides
+// under VALU / MFMA work of the same wave instead of one read-wait-MFMA round trip per
+// MFMA (+32 VGPRs: 3 workgroups per CU instead of 4).
+template <typename K_, bool LAZY, bool VSUM, bool PF>
+__global__ void __launch_bounds__(256, PF ? 3 : 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
   __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
   __shared__ int redo;
@@ -214,12 +218,95 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       if constexpr (!VSUM) osum = K_::mfma32(ones, pf[st], osum);
     }
   };
+  // ---- PF variant of a half tile, in stages
+  auto read_k = [&](int t, int kb, uint4 (&kf)[4]) __attribute__((always_inline)) {
+    const char* K = smem[t & 1];
+    #pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
+  };
+  auto read_v = [&](int t, int kb, uint4 (&vf)[2][2]) __attribute__((always_inline)) {
+    const char* V = smem[t & 1] + TILE_B;
+    #pragma unroll
+    for (int st = 0; st < 2; ++st)
+      #pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int k0 = kb * 32 + 16 * st;
+        const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 0)));
+        const v4s_t up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 1)));
+        const uint2 a = __builtin_bit_cast(uint2, lo), c = __builtin_bit_cast(uint2, up);
+        vf[st][db] = make_uint4(a.x, a.y, c.x, c.y);
+      }
+  };
+  // S^T, (mask), (max), softmax -> pf; then O^T += V^T P^T with the prefetched vf.  `knext`:
+  // the next half's K fragments are read between the softmax and the PV MFMAs.
+  auto half_pf = [&](int t, int kb, const uint4 (&kf)[4], auto partial_tag, bool setmax, bool exact,
+                     bool has_next, int tn, int kbn, uint4 (&knext)[4]) __attribute__((always_inline)) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
+    const int kbase = t * KT;
+    f32x16_t s;
+    #pragma unroll
+    for (int ks = 0; ks < 4; ++ks) s = K_::mfma32(kf[ks], qf[ks], ks == 0 ? f32x16_t{} : s);
+    uint4 vf[2][2];
+    read_v(t, kb, vf);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PARTIAL) {
+      #pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (key >= seq) s[r] = -INFINITY;
+      }
+    }
+    if (setmax) {
+      float mx = fmaxf(s[0], s[1]);
+      #pragma unroll
+      for (int r = 2; r < 16; ++r) mx = fmaxf(mx, s[r]);
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      const float m_new = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
+      if (exact) {
+        if (__builtin_amdgcn_ballot_w64(m_new > m_run + 8.f)) rescale(fmaxf(m_run, m_new));
+      } else {
+        m_run = m_new;
+      }
+    }
+    uint4 pf[2];
+    #pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      uint32_t w[4];
+      #pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj], sl2, -m_run));
+        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
+        w[jj] = K_::pack2(p0, p1);
+        if constexpr (VSUM) lsum += f32x2_t{p0, p1};
+      }
+      pf[st] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (has_next) read_k(tn, kbn, knext);
+    __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      #pragma unroll
+      for (int db = 0; db < 2; ++db) o[db] = K_::mfma32(vf[st][db], pf[st], o[db]);
+      if constexpr (!VSUM) osum = K_::mfma32(ones, pf[st], osum);
+    }
+  };
+
   // a 64-key tile = two halves; the second half of a partial tile is skipped when it holds no key
   auto do_tile = [&](int t, auto partial_tag, bool first, bool exact) __attribute__((always_inline)) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
     if (!active) return;
-    do_half(t, 0, partial_tag, exact || first, exact);
-    if (!PARTIAL || t * KT + 32 < seq) do_half(t, 1, partial_tag, exact, exact);
+    const bool two = !PARTIAL || t * KT + 32 < seq;
+    if constexpr (PF) {
+      uint4 k0[4], k1[4];
+      read_k(t, 0, k0);
+      half_pf(t, 0, k0, partial_tag, exact || first, exact, two, t, 1, k1);
+      if (two) half_pf(t, 1, k1, partial_tag, exact, exact, false, t, 1, k0);
+    } else {
+      do_half(t, 0, partial_tag, exact || first, exact);
+      if (two) do_half(t, 1, partial_tag, exact, exact);
+    }
   };
 
   // One leftover key (seq = 64 n + r, r <= TAIL_VALU: the ViT's 577 = 9 x 64 + 1) costs a
@@ -358,11 +445,18 @@ extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t s
   const float sl2 = (float)((double)scale * 1.4426950408889634);
   hipStream_t s = (hipStream_t)stream;
   // A/B switches: DP_ATTN_LAZY=0 takes the max of every half tile (the exact path);
-  // DP_ATTN_VSUM=0 takes the row sums on the matrix core
+  // DP_ATTN_VSUM=0 takes the row sums on the matrix core; DP_ATTN_PF=1 prefetches the
+  // fragments (3 workgroups per CU).  Measured and rejected (round 2, profiles/r02l_attn_pf/):
+  // 35 x 577 76.9 / 79.5 us prefetched vs 75.4 / 75.3 us (frame 42.50 / 42.71 vs 42.73 / 42.70
+  // fps): the fourth workgroup per CU hides the read latency better than the in-wave prefetch.
   static const bool lazy = [] { const char* e = getenv("DP_ATTN_LAZY"); return !(e && e[0] == '0'); }();
   static const bool vsum = [] { const char* e = getenv("DP_ATTN_VSUM"); return !(e && e[0] == '0'); }();
+  static const bool pf = [] { const char* e = getenv("DP_ATTN_PF"); return e && e[0] == '1'; }();
   if (dtype != DP_BF16 && dtype != DP_F16) return DP_ERR_DTYPE;
-#define DP_ATTN(K, L, V) hipLaunchKernelGGL((attn_kernel<K, L, V>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2)
+#define DP_ATTN(K, L, V) do { \
+    if (pf) hipLaunchKernelGGL((attn_kernel<K, L, V, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2); \
+    else hipLaunchKernelGGL((attn_kernel<K, L, V, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2); \
+  } while (0)
 #define DP_ATTN_K(K)                                                               \
   do {                                                                             \
     if (lazy) { if (vsum) DP_ATTN(K, true, true); else DP_ATTN(K, true, false); }  \
