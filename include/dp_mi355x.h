@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 5
+#define DP_ABI_VERSION 6
 int dp_abi_version(void);
 
 /*
@@ -189,6 +189,15 @@ int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, vo
  */
 int dp_attention(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
                  int32_t head_dim, float scale, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_attention_log2q: dp_attention for a qkv whose Q columns already hold
+ * Q * scale * log2(e) -- folded into the qkv Linear's epilogue as a per-column gamma --
+ * so the scores leave the MFMA in log2 units and the softmax needs one exp2 per score.
+ * Same result as dp_attention up to where the scale is rounded (before the 16-bit Q).
+ */
+int dp_attention_log2q(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
+                       int32_t head_dim, int32_t dtype, dp_stream_t stream);
 
 /*
  * dp_normalize_u8: uint8 HWC image -> (x/255 - 0.5)/0.5 planar CHW (fp32 or 16-bit).

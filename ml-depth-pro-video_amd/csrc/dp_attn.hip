@@ -70,7 +70,11 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
 // softmax and the next half's K fragments before its PV MFMAs, so their LDS latency hides
 // under VALU / MFMA work of the same wave instead of one read-wait-MFMA round trip per
 // MFMA (+32 VGPRs: 3 workgroups per CU instead of 4).
-template <typename K_, bool LAZY, bool VSUM, bool PF>
+// PRE: the Q columns of qkv already hold Q * scale * log2(e) (dp_attention_log2q: the qkv
+// GEMM's per-column gamma), so scores come out of the MFMA in log2 units; once the lazy
+// running max is set, the S^T accumulator starts at -m_run instead of 0 and P = 2^S^T is ONE
+// v_exp_f32 per score (no v_fma_f32: a quarter of the softmax's VALU issue).
+template <typename K_, bool LAZY, bool VSUM, bool PF, bool PRE = false>
 __global__ void __launch_bounds__(256, PF ? 3 : 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
   __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
@@ -164,11 +168,18 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     const int kbase = t * KT;
     const char* K = smem[cur];
     const char* V = smem[cur] + TILE_B;
+    // PRE, lazy max already set: the accumulator carries -m_run, P = 2^S directly
+    const bool off = PRE && !setmax && !exact;
     f32x16_t s;
     #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const uint4 kf = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
-      s = K_::mfma32(kf, qf[ks], ks == 0 ? f32x16_t{} : s);
+      f32x16_t c0 = f32x16_t{};
+      if (off) {
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) c0[r] = -m_run;
+      }
+      s = K_::mfma32(kf, qf[ks], ks == 0 ? c0 : s);
     }
     if constexpr (PARTIAL) {
       #pragma unroll
@@ -196,8 +207,14 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       uint32_t w[4];
       #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj], sl2, -m_run));
-        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
+        float p0, p1;
+        if (off) {
+          p0 = __builtin_amdgcn_exp2f(s[8 * st + 2 * jj]);
+          p1 = __builtin_amdgcn_exp2f(s[8 * st + 2 * jj + 1]);
+        } else {
+          p0 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj], sl2, -m_run));
+          p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
+        }
         w[jj] = K_::pack2(p0, p1);
         if constexpr (VSUM) lsum += f32x2_t{p0, p1};
       }
@@ -431,8 +448,9 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
 
 }  // namespace
 
-extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
-                            int32_t head_dim, float scale, int32_t dtype, dp_stream_t stream) {
+namespace {
+int attention_launch(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads, int32_t head_dim,
+                     float scale, bool pre, int32_t dtype, dp_stream_t stream) {
   if (!qkv || !out) return DP_ERR_ARG;
   if (batch <= 0 || seq <= 0 || heads <= 0 || head_dim != HD) return DP_ERR_SHAPE;
   // Measured and rejected (35 x 577): two independent 32-query sub-blocks per wave (K / V
@@ -442,7 +460,7 @@ extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t s
   if ((long long)nq * heads * batch > 0x7fffffffLL) return DP_ERR_SHAPE;
   dim3 grid(nq * heads * batch);
   // softmax(s * scale) = 2^(s * scale * log2 e) / sum: sl2 is the scale in log2 units
-  const float sl2 = (float)((double)scale * 1.4426950408889634);
+  const float sl2 = pre ? 1.0f : (float)((double)scale * 1.4426950408889634);
   hipStream_t s = (hipStream_t)stream;
   // A/B switches: DP_ATTN_LAZY=0 takes the max of every half tile (the exact path);
   // DP_ATTN_VSUM=0 takes the row sums on the matrix core; DP_ATTN_PF=1 prefetches the
@@ -462,10 +480,27 @@ extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t s
     if (lazy) { if (vsum) DP_ATTN(K, true, true); else DP_ATTN(K, true, false); }  \
     else { if (vsum) DP_ATTN(K, false, true); else DP_ATTN(K, false, false); }     \
   } while (0)
-  if (dtype == DP_BF16) DP_ATTN_K(KBF16);
-  else DP_ATTN_K(KF16);
+  if (pre) {   // the default kernel (lazy max, VALU row sums) with log2-unit Q
+    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+  } else if (dtype == DP_BF16) {
+    DP_ATTN_K(KBF16);
+  } else {
+    DP_ATTN_K(KF16);
+  }
 #undef DP_ATTN_K
 #undef DP_ATTN
   DP_CHECK_LAUNCH();
   return 0;
+}
+}  // namespace
+
+extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
+                            int32_t head_dim, float scale, int32_t dtype, dp_stream_t stream) {
+  return attention_launch(qkv, out, batch, seq, heads, head_dim, scale, false, dtype, stream);
+}
+
+extern "C" int dp_attention_log2q(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
+                                  int32_t head_dim, int32_t dtype, dp_stream_t stream) {
+  return attention_launch(qkv, out, batch, seq, heads, head_dim, 1.0f, true, dtype, stream);
 }

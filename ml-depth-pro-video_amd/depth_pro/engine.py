@@ -317,6 +317,10 @@ class Engine:
         self.side_streams = int(os.environ.get("DP_SIDE_STREAMS", "2"))
         # GEMM engine of the side encoders' block GEMMs (DP_SIDE_TILE, a DP_TILE_* value; 0 = planner)
         self.side_tile = int(os.environ.get("DP_SIDE_TILE", "0"))
+        # softmax scale * log2(e) folded into the qkv epilogue (per-column gamma on Q) so that attention
+        # takes one exp2 per score (dp_attention_log2q); DP_ATTN_LOG2Q=0: scale inside the attention
+        self.qkv_gamma = (ops.log2q_gamma(HEADS, D // HEADS, dev)
+                          if os.environ.get("DP_ATTN_LOG2Q", "1") == "1" else None)
         # ViT LayerNorms fused into the patch encoder's proj / fc2 epilogues (dp_gemm_ln, DP_LN_FUSE=1).
         # Measured and rejected (round 2, profiles/r02k_ln_fuse/): 40.35 / 40.44 fps fused vs 41.84 /
         # 41.73 separate; eager proj + LN 100.6 us fused vs 67.8 + 22.5, fc2 + LN 194.2 vs 169.8 + 22.5:
@@ -350,9 +354,9 @@ class Engine:
                 ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"],
-                         tile=t)
+                         gamma=self.qkv_gamma, tile=t)
             if "attn" not in _ABLATE:
-                ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS)
+                ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=self.qkv_gamma is not None)
             ln2 = (P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, 1e-6) if fuse else None
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],

@@ -240,10 +240,27 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor
 
 
 def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int = 16,
-              head_dim: int = 64) -> None:
+              head_dim: int = 64, log2q: bool = False) -> None:
+    """dp_attention; `log2q=True`: dp_attention_log2q, the Q columns of `qkv` already hold
+    Q * head_dim^-0.5 * log2(e) (see `log2q_gamma`)."""
     with _Timed("attention", 4.0 * batch * heads * seq * seq * head_dim, (batch, seq), out.dtype):
-        check(_lib.load().dp_attention(qkv.data_ptr(), out.data_ptr(), batch, seq, heads, head_dim,
-                                       head_dim ** -0.5, dtype_code(out.dtype), _stream(out)), "dp_attention")
+        if log2q:
+            check(_lib.load().dp_attention_log2q(qkv.data_ptr(), out.data_ptr(), batch, seq, heads, head_dim,
+                                                 dtype_code(out.dtype), _stream(out)), "dp_attention_log2q")
+        else:
+            check(_lib.load().dp_attention(qkv.data_ptr(), out.data_ptr(), batch, seq, heads, head_dim,
+                                           head_dim ** -0.5, dtype_code(out.dtype), _stream(out)), "dp_attention")
+
+
+LOG2E = 1.4426950408889634
+
+
+def log2q_gamma(heads: int, head_dim: int, device) -> torch.Tensor:
+    """Per-column gamma for the qkv Linear's epilogue that leaves Q scaled by head_dim^-0.5 *
+    log2(e) (the softmax scale in log2 units) and K, V unchanged: input of dp_attention_log2q."""
+    g = torch.ones(3 * heads * head_dim, dtype=torch.float32)
+    g[:heads * head_dim] = float(head_dim ** -0.5 * LOG2E)
+    return g.to(device)
 
 
 def normalize_u8(img: torch.Tensor, out: torch.Tensor) -> None:

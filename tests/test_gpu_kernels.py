@@ -144,12 +144,17 @@ def test_head_conv_with_fused_1x1(cuda, dt):
                                              (2, 66, None), (1, 2, None), (1, 67, None),
                                              (2, 577, "tail"), (1, 130, "tail"), (2, 577, "mid"),
                                              (1, 100, "mid")])
-def test_attention(cuda, dt, batch, seq, spike):
+@pytest.mark.parametrize("log2q", [False, True])
+def test_attention(cuda, dt, batch, seq, spike, log2q):
     """seq 577 / 66 / 2 / 130 end in 1-2 leftover keys (the VALU tail), 100 / 67 in a partial
     MFMA tile.  spike "tail": the LAST key of every sequence is the scaled query of token 0, so
     that query's running max jumps inside the tail -- the rescale branch there is exercised;
     "mid": key 70 (second key tile) is 40x that query, far above the max the first half key
-    tile set: P overflows and the workgroup redoes its keys on the exact-max path."""
+    tile set: P overflows and the workgroup redoes its keys on the exact-max path.
+    log2q: dp_attention_log2q on the same qkv with its Q columns pre-multiplied by
+    hd^-0.5 * log2(e) and rounded to 16 bits (what the engine's qkv epilogue writes); the fp32
+    reference takes its Q from those rounded values (in the model Q is rounded once either way:
+    the test's second rounding would otherwise move the 40x spike's scores by ~0.5 log2 units)."""
     g = torch.Generator().manual_seed(seq)
     H, hd = 16, 64
     qkv = rnd(batch * seq, 3 * H * hd, dt=dt, dev=cuda, gen=g, scale=2.0)
@@ -157,10 +162,17 @@ def test_attention(cuda, dt, batch, seq, spike):
         x = qkv.view(batch, seq, 3, H, hd)
         key, f = (seq - 1, 4.0) if spike == "tail" else (70, 40.0)
         x[:, key, 1] = (x[:, 0, 0].float() * f).to(dt)
+    if log2q:
+        g2 = ops.log2q_gamma(H, hd, cuda)
+        qkv_in = (qkv.float() * g2).to(dt)
+        qkv = qkv_in.float() / g2          # fp32: the reference sees exactly the rounded Q
     q, k, v = qkv.float().reshape(batch, seq, 3, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
     ref = F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(batch * seq, H * hd)
     out = torch.empty(batch * seq, H * hd, dtype=dt, device=cuda)
-    ops.attention(qkv, out, batch, seq, H, hd)
+    if log2q:
+        ops.attention(qkv_in, out, batch, seq, H, hd, log2q=True)
+    else:
+        ops.attention(qkv, out, batch, seq, H, hd)
     close(out, ref, dt, "attention")
 
 

@@ -1,2 +1,4 @@
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && O=gpurun_out/r02m && mkdir -p $O && \
-for T in 0 12 4 0 12 4; do DP_SIDE_TILE=$T timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $O/b.json 2> $O/b.err || exit 1; echo "{\"side_tile\": $T, \"r\": $(cat $O/b.json)}" >> $O/all.jsonl; done
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && O=gpurun_out/r02o && mkdir -p $O && \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q -k attention --timeout 120 --timeout-method thread > $O/t_attn.log 2>&1 && \
+for L in 1 0 1 0; do DP_ATTN_LOG2Q=$L timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $O/b.json 2> $O/b.err || exit 1; echo "{\"log2q\": $L, \"r\": $(cat $O/b.json)}" >> $O/all.jsonl; done && \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py -x -q --timeout 300 --timeout-method thread > $O/t_model.log 2>&1
