@@ -74,7 +74,11 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
 // GEMM's per-column gamma), so scores come out of the MFMA in log2 units; once the lazy
 // running max is set, the S^T accumulator starts at -m_run instead of 0 and P = 2^S^T is ONE
 // v_exp_f32 per score (no v_fma_f32: a quarter of the softmax's VALU issue).
-template <typename K_, bool LAZY, bool VSUM, bool PF, bool PRE = false>
+// SADD (with VSUM): the row sums as ONE serial chain of v_add_f32 (nothing independent and
+// isomorphic for the compiler to SLP-pack into v_pk_add_f32, which costs more issue beside
+// MFMAs).  Not inline asm: an asm add that reads a v_exp_f32 result right away misses the
+// transcendental-use wait state the compiler inserts for its own instructions.
+template <typename K_, bool LAZY, bool VSUM, bool PF, bool PRE = false, bool SADD = false>
 __global__ void __launch_bounds__(256, PF ? 3 : 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
   __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
@@ -142,6 +146,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
 
   f32x16_t o[2], osum;         // osum (!VSUM): row sums of P from an all-ones A operand
   f32x2_t lsum;                // VSUM: this lane's share of its query's row sum (its 32 of 64 keys)
+  float ls4[4];                // SADD: the same share as four partial sums
   float m_run;
   const uint32_t one2 = K_::pack2(1.f, 1.f);
   const uint4 ones = make_uint4(one2, one2, one2, one2);
@@ -154,6 +159,10 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       if constexpr (!VSUM) osum[i] *= alpha;
     }
     if constexpr (VSUM) lsum *= alpha;
+    if constexpr (SADD) {
+      #pragma unroll
+      for (int i = 0; i < 4; ++i) ls4[i] *= alpha;
+    }
     m_run = m_upd;
   };
 
@@ -216,7 +225,11 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
           p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
         }
         w[jj] = K_::pack2(p0, p1);
-        if constexpr (VSUM) lsum += f32x2_t{p0, p1};
+        if constexpr (SADD) {
+          ls4[0] = (ls4[0] + p0) + p1;
+        } else if constexpr (VSUM) {
+          lsum += f32x2_t{p0, p1};
+        }
       }
       pf[st] = make_uint4(w[0], w[1], w[2], w[3]);
     }
@@ -355,6 +368,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     const float pr = __builtin_amdgcn_exp2f(sc - m_run);
     const float p = K_::to_f(K_::from_f(pr));
     if constexpr (!VSUM) osum[0] += p;
+    else if constexpr (SADD) ls4[0] += 0.5f * p;
     else lsum[0] += 0.5f * p;   // both half-waves add it: the swap below doubles it
     #pragma unroll
     for (int db = 0; db < 2; ++db)
@@ -379,6 +393,8 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     #pragma unroll
     for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; osum[i] = 0.f; }
     lsum = f32x2_t{0.f, 0.f};
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) ls4[i] = 0.f;
     m_run = -INFINITY;
     if (nmma > 0) issue(0, 0);
     if (nfull > 0) {
@@ -401,7 +417,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   };
   auto row_sum = [&]() __attribute__((always_inline)) {
     if constexpr (VSUM) {
-      const float l = lsum[0] + lsum[1];
+      const float l = SADD ? (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]) : lsum[0] + lsum[1];
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
       return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
     } else {
@@ -480,9 +496,16 @@ int attention_launch(const void* qkv, void* out, int32_t batch, int32_t seq, int
     if (lazy) { if (vsum) DP_ATTN(K, true, true); else DP_ATTN(K, true, false); }  \
     else { if (vsum) DP_ATTN(K, false, true); else DP_ATTN(K, false, false); }     \
   } while (0)
+  // DP_ATTN_SADD=0: packed row-sum adds in the log2q kernel (A/B)
+  static const bool sadd = [] { const char* e = getenv("DP_ATTN_SADD"); return !(e && e[0] == '0'); }();
   if (pre) {   // the default kernel (lazy max, VALU row sums) with log2-unit Q
-    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-    else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    if (sadd) {
+      if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+      else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    } else {
+      if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+      else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    }
   } else if (dtype == DP_BF16) {
     DP_ATTN_K(KBF16);
   } else {
