@@ -371,8 +371,10 @@ __device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc
       #pragma unroll
       for (int r = 0; r < 8; ++r) x[r] = gelu_erf(x[r]);
     }
-    #pragma unroll
-    for (int r = 0; r < 8; ++r) x[r] *= cc.g[r];
+    if (p.gamma) {
+      #pragma unroll
+      for (int r = 0; r < 8; ++r) x[r] *= cc.g[r];
+    }
     if (p.pos) add8_f32(x, p.pos + (long long)(mc[it] % p.pos_group + p.pos_off) * p.ldpos + nc);
     if (p.R1) add8_u4<K_>(x, r1[it]);
     if (p.R2) add8_u4<K_>(x, r2[it]);
@@ -448,8 +450,10 @@ __device__ __forceinline__ void epilogue_rows_buf(const GemmP& p, const ColConst
       #pragma unroll
       for (int r = 0; r < 8; ++r) x[r] = gelu_erf(x[r]);
     }
-    #pragma unroll
-    for (int r = 0; r < 8; ++r) x[r] *= cc.g[r];
+    if (p.gamma) {
+      #pragma unroll
+      for (int r = 0; r < 8; ++r) x[r] *= cc.g[r];
+    }
     if (p.pos) add8_f32(x, p.pos + (long long)(mc[it] % p.pos_group + p.pos_off) * p.ldpos + nc);
     if (p.R1) add8_u4<K_>(x, r1[it]);
     if (p.R2) add8_u4<K_>(x, r2[it]);
@@ -531,7 +535,8 @@ __device__ __forceinline__ void head_ps_rows(const GemmP& p, const ColConst& cc,
 // distinct A / B panels in its 4 MiB L2: qkv 155 -> 150 us, fc1 197 -> 190 us
 // (tools/gemm_bench.py --dbg 16 restores row-major, for A/B).
 __device__ __forceinline__ void tile_coords(const GemmP& p, int wgid, int& tile_m, int& tile_n) {
-  const int band = (p.dbg & 16) ? 1 : 4;
+  // debug 16: row-major; 1 << 18: bands of 8 rows; 1 << 19: bands of 2 rows (A/B)
+  const int band = (p.dbg & 16) ? 1 : (p.dbg & (1 << 18)) ? 8 : (p.dbg & (1 << 19)) ? 2 : 4;
   const int tm_full = p.tiles_m / band * band;       // rows covered by whole bands
   const int per_band = band * p.tiles_n;
   if (band > 1 && wgid < tm_full * p.tiles_n) {
@@ -715,6 +720,10 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   for (int i = 0; i < FM; ++i)
     #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // debug 1 << 17 (A/B): static priority -- waves 4-7 (the arbitration losers of each SIMD pair)
+  // at priority 1 for the whole loop instead of a raise / drop around every MFMA group
+  const bool sprio = p.dbg & (1 << 17);
+  if (sprio && wave_u >= 4) __builtin_amdgcn_s_setprio(1);
 
   const int frow = lane & 15, fchunk = lane >> 4;
   constexpr int KS = BKT / 32;
@@ -733,7 +742,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       uint4 afs[FM];
       #pragma unroll
       for (int i = 0; i < FM; ++i) afs[i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
-      __builtin_amdgcn_s_setprio(1);
+      if (!sprio) __builtin_amdgcn_s_setprio(1);
       #pragma unroll
       for (int i = 0; i < FM; ++i) {
         uint4 af = afs[i];
@@ -741,7 +750,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
         #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
       }
-      __builtin_amdgcn_s_setprio(0);
+      if (!sprio) __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -795,7 +804,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
         fa[i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
     };
     auto mma = [&](const uint4 (&fa)[FM], const uint4 (&fb)[FN]) {
-      __builtin_amdgcn_s_setprio(1);
+      if (!sprio) __builtin_amdgcn_s_setprio(1);
       #pragma unroll
       for (int i = 0; i < FM; ++i) {
         uint4 a = fa[i];
@@ -803,7 +812,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
         #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(fb[j], a, acc[i][j]);
       }
-      __builtin_amdgcn_s_setprio(0);
+      if (!sprio) __builtin_amdgcn_s_setprio(0);
     };
     #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
@@ -862,6 +871,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
   }
 
   DP_STAMP(st2_);
+  if (sprio) __builtin_amdgcn_s_setprio(0);
   if (p.dbg & 1) {
     #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -1412,10 +1422,12 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
       for (int fn = 0; fn < 2; ++fn)
         bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((wn & 1) * 64 + qn * 32 + fn * 16 + frow, ks * 4 + fchunk));
   };
+  const bool sprio = p.dbg & (1 << 17);   // A/B: static priority for waves 4-7 (see gemm_big_kernel)
+  if (sprio && wave_u >= 4) __builtin_amdgcn_s_setprio(1);
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    if (!sprio) __builtin_amdgcn_s_setprio(1);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
@@ -1426,7 +1438,7 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
         for (int fn = 0; fn < 2; ++fn)
           acc[qm * 4 + fm][qn * 2 + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * 2 + fn]);
       }
-    __builtin_amdgcn_s_setprio(0);
+    if (!sprio) __builtin_amdgcn_s_setprio(0);
   };
   auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
 
@@ -1467,6 +1479,7 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
     bar();
   }
   if (wm == 0) bar();
+  if (sprio) __builtin_amdgcn_s_setprio(0);
 
   // epilogue: identical to the big engine (LDS-staged, row-coalesced)
   lds_barrier();

@@ -287,13 +287,19 @@ class Engine:
         self.ws_main = ops.gemm_workspace(dev)
         self.ws_side = ops.gemm_workspace(dev)
         self.ws_side2 = ops.gemm_workspace(dev)
+        # project/upsample chains and the decoder's encoder-feature projections beside the main
+        # stream (DP_DEC_STREAMS=1, see _forward): two more streams, one of them issuing stream-K
+        self.dec_a = torch.cuda.Stream(device=dev)
+        self.dec_b = torch.cuda.Stream(device=dev)
+        self.ws_dec = ops.gemm_workspace(dev)
+        self.dec_streams = os.environ.get("DP_DEC_STREAMS", "1") == "1"
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
         # `DP_PATCH_GROUPS` window groups on their own streams, so one group's bandwidth-bound
         # phases (LayerNorm, GEMM epilogues) overlap another group's MFMA phases.
         self.set_patch_groups(int(os.environ.get("DP_PATCH_GROUPS", "1")), _init=True)
         # their sticky error words (dp_mi355x.h DP_GEMM_WS_ERROR_OFFSET), read back asynchronously
         # after every forward into pinned memory and checked by `check_status`
-        wss = [self.ws_main, self.ws_side, self.ws_side2] + self.ws_groups
+        wss = [self.ws_main, self.ws_side, self.ws_side2, self.ws_dec] + self.ws_groups
         self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32) for w in wss]
         self._err_host = torch.zeros(len(wss), dtype=torch.int32, pin_memory=True)
         self._err_ev: Optional[torch.cuda.Event] = None
@@ -421,7 +427,7 @@ class Engine:
         self.ws_groups = [ops.gemm_workspace(self.dev) for _ in self.patch_groups[1:]]
         if not _init:
             self.graph = None
-            wss = [self.ws_main, self.ws_side, self.ws_side2] + self.ws_groups
+            wss = [self.ws_main, self.ws_side, self.ws_side2, self.ws_dec] + self.ws_groups
             self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32) for w in wss]
             self._err_host = torch.zeros(len(wss), dtype=torch.int32, pin_memory=True)
             self._err_ev = None
@@ -532,13 +538,30 @@ class Engine:
             side_encoders()
         # project / upsample (encoder.py:314-324)
         e = "encoder."
-        ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
-        self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
-        self._deconv(self.t192_256, 192, 256, P[e + "upsample_latent0.2"], self.t384_256, 256)
-        self._deconv(self.t384_256, 384, 256, P[e + "upsample_latent0.3"], self.enc0, 256)
-        ops.gemm(self.lat1, P[e + "upsample_latent1.0"], self.t96_256b, M=96 * 96, N=256, K=D)
-        self._deconv(self.t96_256b, 96, 256, P[e + "upsample_latent1.1"], self.t192_256b, 256)
-        self._deconv(self.t192_256b, 192, 256, P[e + "upsample_latent1.2"], self.enc1, 256)
+        par = self.dec_streams and not serial and not fov_side
+
+        def lat0_chain():
+            ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
+            self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
+            self._deconv(self.t192_256, 192, 256, P[e + "upsample_latent0.2"], self.t384_256, 256)
+            self._deconv(self.t384_256, 384, 256, P[e + "upsample_latent0.3"], self.enc0, 256)
+
+        def lat1_chain():
+            ops.gemm(self.lat1, P[e + "upsample_latent1.0"], self.t96_256b, M=96 * 96, N=256, K=D)
+            self._deconv(self.t96_256b, 96, 256, P[e + "upsample_latent1.1"], self.t192_256b, 256)
+            self._deconv(self.t192_256b, 192, 256, P[e + "upsample_latent1.2"], self.enc1, 256)
+
+        if par:
+            # The two latent chains (small grids, ~0.4 ms in a row) beside the main stream's f0 / f1
+            # / f2 chains.  Side streams issue no stream-K launch that could overlap one of the main
+            # stream's (workgroups that wait on each other, dp_mi355x.h): no workspace here.
+            for st, chain in ((self.dec_a, lat0_chain), (self.dec_b, lat1_chain)):
+                st.wait_stream(main)
+                with torch.cuda.stream(st), ops.use_workspace(None):
+                    chain()
+        else:
+            lat0_chain()
+            lat1_chain()
         ops.gemm(self.f0, P[e + "upsample0.0"], self.t96_512, M=96 * 96, N=512, K=D)
         self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
         ops.gemm(self.f1, P[e + "upsample1.0"], self.t48_1024, M=48 * 48, N=D, K=D)
@@ -550,7 +573,27 @@ class Engine:
         ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
         self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)
-        if self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
+        if par:
+            # FOV head (fov.py:56-82; needs only the low-res features) on the FOV encoder's stream,
+            # off the main stream's critical path (its 24^2 - 6^2 convs leave the chip idle)
+            if self.use_fov:
+                self.side2.wait_stream(main)
+                with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
+                    self._fov_head()
+            # convs.3 / .2 / .1 (the encoder features' projections, decoder.py:74-93) on dec_a in
+            # the order the fusions need them, each beside the previous fusion block: after
+            # convs.4 (the main stream's last stream-K launch before fusion 1's deconv, which
+            # waits for convs.1), so dec_a's stream-K launches never overlap the main stream's
+            self.dec_a.wait_stream(main)
+            self.dec_a.wait_stream(self.dec_b)      # enc1 (lat1 chain) for convs.1
+            evs = {}
+            with torch.cuda.stream(self.dec_a), ops.use_workspace(self.ws_dec):
+                for i, (enc, s_, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)),
+                                          (1, (self.enc1, 384, 256))):
+                    self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256)
+                    evs[i] = torch.cuda.Event()
+                    evs[i].record(self.dec_a)
+        elif self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
             if self.side_streams == 2 and not serial:
                 main.wait_stream(self.side2)
             self._fov_head()
@@ -564,11 +607,21 @@ class Engine:
             f = self._fusion(4, self.low, 48, None)
             for i, (enc, s, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)), (1, (self.enc1, 384, 256))):
                 c = self.dec[s]["c"]
-                self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
+                if par:
+                    main.wait_event(evs[i])
+                else:
+                    self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
                 f = self._fusion(i, f, s, c)
+            if par:
+                main.wait_stream(self.dec_a)        # enc0 (lat0 chain) for fusion 0
             feats = self._fusion(0, f, 768, self.enc0)
         else:
             feats = self.feats
+        if par:
+            main.wait_stream(self.dec_a)
+            main.wait_stream(self.dec_b)
+            if self.use_fov:
+                main.wait_stream(self.side2)
         if fov_side:
             main.wait_stream(self.side)
         if "head" in _ABLATE:
@@ -627,7 +680,7 @@ class Engine:
         self._err_ev = None
         if int(self._err_host.abs().sum()) != 0:
             self._err_host.zero_()
-            for w in [self.ws_main, self.ws_side, self.ws_side2] + self.ws_groups:
+            for w in [self.ws_main, self.ws_side, self.ws_side2, self.ws_dec] + self.ws_groups:
                 w.zero_()   # error word, and any hand-off flag the timed-out launch left set
             raise DPError("dp_gemm: a stream-K partial-tile or fused-LayerNorm row-band hand-off timed out; "
                           "the depth map of a recent frame is invalid (workspace error word set)")
