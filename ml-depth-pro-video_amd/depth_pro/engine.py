@@ -291,6 +291,7 @@ class Engine:
         # stream (DP_DEC_STREAMS=1, see _forward): two more streams, one of them issuing stream-K
         self.dec_a = torch.cuda.Stream(device=dev)
         self.dec_b = torch.cuda.Stream(device=dev)
+        self.dec_c = torch.cuda.Stream(device=dev)
         self.ws_dec = ops.gemm_workspace(dev)
         self.dec_streams = os.environ.get("DP_DEC_STREAMS", "1") == "1"
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
@@ -551,21 +552,34 @@ class Engine:
             self._deconv(self.t96_256b, 96, 256, P[e + "upsample_latent1.1"], self.t192_256b, 256)
             self._deconv(self.t192_256b, 192, 256, P[e + "upsample_latent1.2"], self.enc1, 256)
 
+        def f1_chain():
+            ops.gemm(self.f1, P[e + "upsample1.0"], self.t48_1024, M=48 * 48, N=D, K=D)
+            self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
+
+        def f0_chain():
+            ops.gemm(self.f0, P[e + "upsample0.0"], self.t96_512, M=96 * 96, N=512, K=D)
+            self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
+
+        enc_ev = {}
         if par:
-            # The two latent chains (small grids, ~0.4 ms in a row) beside the main stream's f0 / f1
-            # / f2 chains.  Side streams issue no stream-K launch that could overlap one of the main
-            # stream's (workgroups that wait on each other, dp_mi355x.h): no workspace here.
-            for st, chain in ((self.dec_a, lat0_chain), (self.dec_b, lat1_chain)):
+            # The latent chains and the f0 / f1 chains (small grids, ~0.6 ms in a row) beside the
+            # main stream's f2 chain -> fuse_lowres -> convs.4, in the order the decoder's
+            # projections need their outputs (enc3, enc2, enc1; enc0 last).  Side streams issue no
+            # stream-K launch that could overlap one of the main stream's (workgroups that wait on
+            # each other, dp_mi355x.h): no workspace here.
+            for st, chains in ((self.dec_a, (("enc0", lat0_chain),)),
+                               (self.dec_b, (("enc3", f1_chain), ("enc2", f0_chain), ("enc1", lat1_chain)))):
                 st.wait_stream(main)
                 with torch.cuda.stream(st), ops.use_workspace(None):
-                    chain()
+                    for name, chain in chains:
+                        chain()
+                        enc_ev[name] = torch.cuda.Event()
+                        enc_ev[name].record(st)
         else:
             lat0_chain()
             lat1_chain()
-        ops.gemm(self.f0, P[e + "upsample0.0"], self.t96_512, M=96 * 96, N=512, K=D)
-        self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
-        ops.gemm(self.f1, P[e + "upsample1.0"], self.t48_1024, M=48 * 48, N=D, K=D)
-        self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
+            f0_chain()
+            f1_chain()
         ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
         if not serial:
@@ -580,19 +594,19 @@ class Engine:
                 self.side2.wait_stream(main)
                 with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
                     self._fov_head()
-            # convs.3 / .2 / .1 (the encoder features' projections, decoder.py:74-93) on dec_a in
+            # convs.3 / .2 / .1 (the encoder features' projections, decoder.py:74-93) on dec_c in
             # the order the fusions need them, each beside the previous fusion block: after
             # convs.4 (the main stream's last stream-K launch before fusion 1's deconv, which
-            # waits for convs.1), so dec_a's stream-K launches never overlap the main stream's
-            self.dec_a.wait_stream(main)
-            self.dec_a.wait_stream(self.dec_b)      # enc1 (lat1 chain) for convs.1
+            # waits for convs.1), so dec_c's stream-K launches never overlap the main stream's
+            self.dec_c.wait_stream(main)
             evs = {}
-            with torch.cuda.stream(self.dec_a), ops.use_workspace(self.ws_dec):
+            with torch.cuda.stream(self.dec_c), ops.use_workspace(self.ws_dec):
                 for i, (enc, s_, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)),
                                           (1, (self.enc1, 384, 256))):
+                    self.dec_c.wait_event(enc_ev[f"enc{i}"])
                     self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256)
                     evs[i] = torch.cuda.Event()
-                    evs[i].record(self.dec_a)
+                    evs[i].record(self.dec_c)
         elif self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
             if self.side_streams == 2 and not serial:
                 main.wait_stream(self.side2)
@@ -613,13 +627,14 @@ class Engine:
                     self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
                 f = self._fusion(i, f, s, c)
             if par:
-                main.wait_stream(self.dec_a)        # enc0 (lat0 chain) for fusion 0
+                main.wait_event(enc_ev["enc0"])     # lat0 chain for fusion 0
             feats = self._fusion(0, f, 768, self.enc0)
         else:
             feats = self.feats
         if par:
             main.wait_stream(self.dec_a)
             main.wait_stream(self.dec_b)
+            main.wait_stream(self.dec_c)
             if self.use_fov:
                 main.wait_stream(self.side2)
         if fov_side:
