@@ -294,6 +294,8 @@ class Engine:
         self.dec_c = torch.cuda.Stream(device=dev)
         self.ws_dec = ops.gemm_workspace(dev)
         self.dec_streams = os.environ.get("DP_DEC_STREAMS", "1") == "1"
+        self.small_conv_tile = int(os.environ.get("DP_SMALL_CONV_TILE", "0"))
+        self.fov_at = int(os.environ.get("DP_FOV_AT", "-1"))
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
         # `DP_PATCH_GROUPS` window groups on their own streams, so one group's bandwidth-bound
         # phases (LayerNorm, GEMM epilogues) overlap another group's MFMA phases.
@@ -389,10 +391,13 @@ class Engine:
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
                stride=1, head_w=None, head_b=0.0):
         s_out = (s_in + 2 - 3) // stride + 1
+        # A/B (DP_SMALL_CONV_TILE, a DP_TILE_* value): engine of the decoder's small-grid
+        # ResidualBlock convs (48^2 / 96^2: 9 / 36 tiles of 256 x 256 on 256 CUs)
+        tile = self.small_conv_tile if (self.small_conv_tile and s_out <= 96 and cout == 256 and cin == 256) else 0
         ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
                  conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
                  relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout,
-                 head_w=head_w, head_b=head_b, ldc=cout)
+                 head_w=head_w, head_b=head_b, ldc=cout, tile=tile)
 
     def _deconv(self, x, s_in, cin, w, out, cout, bias=None, C_off=0, ldc=None):
         ops.gemm(x, w, out, M=s_in * s_in, N=4 * cout, K=cin, bias=bias, deconv=(s_in, s_in, cout),
@@ -515,12 +520,19 @@ class Engine:
                 if side_ok:
                     if self.use_fov and not fov_side and self.side_streams == 1:
                         self._fov_encoder()
-            if self.use_fov and not fov_side and self.side_streams == 2:
-                self.side2.wait_stream(main)
-                with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
-                    if side_ok and "fovenc" not in _ABLATE:
-                        self._fov_encoder()
+            if self.use_fov and not fov_side and self.side_streams == 2 and fov_at < 0:
+                fov_encoder_side2()
 
+        def fov_encoder_side2():
+            self.side2.wait_stream(main)
+            with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
+                if side_ok and "fovenc" not in _ABLATE:
+                    self._fov_encoder()
+
+        # DP_FOV_AT=b (A/B): start the FOV encoder after patch-encoder block b instead of with the
+        # image encoder (it is needed only at the FOV head, after the decoder's first conv)
+        fov_at = self.fov_at if (self.use_fov and not fov_side and self.side_streams == 2 and not serial
+                                 and len(self.patch_groups) == 1) else -1
         if self.side_mode != "late" or serial:
             side_encoders()
         vp = self.vp
@@ -529,6 +541,9 @@ class Engine:
                 5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
                 11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
             }
+            if fov_at >= 0:
+                prev = hooks.get(fov_at)
+                hooks[fov_at] = (lambda: (prev(), fov_encoder_side2())) if prev else fov_encoder_side2
             self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True)
         else:
             self._patch_groups(main)
