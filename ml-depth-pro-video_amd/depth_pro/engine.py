@@ -296,6 +296,7 @@ class Engine:
         self.dec_streams = os.environ.get("DP_DEC_STREAMS", "1") == "1"
         self.small_conv_tile = int(os.environ.get("DP_SMALL_CONV_TILE", "0"))
         self.fov_at = int(os.environ.get("DP_FOV_AT", "-1"))
+        self.lat0_sk = os.environ.get("DP_LAT0_SK", "1") == "1"
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
         # `DP_PATCH_GROUPS` window groups on their own streams, so one group's bandwidth-bound
         # phases (LayerNorm, GEMM epilogues) overlap another group's MFMA phases.
@@ -556,11 +557,17 @@ class Engine:
         e = "encoder."
         par = self.dec_streams and not serial and not fov_side
 
-        def lat0_chain():
+        def lat0_pre():
             ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
             self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
             self._deconv(self.t192_256, 192, 256, P[e + "upsample_latent0.2"], self.t384_256, 256)
+
+        def lat0_last():   # 384^2 -> 768^2: 2304 tiles of K = 256, the stream-K engine's best case
             self._deconv(self.t384_256, 384, 256, P[e + "upsample_latent0.3"], self.enc0, 256)
+
+        def lat0_chain():
+            lat0_pre()
+            lat0_last()
 
         def lat1_chain():
             ops.gemm(self.lat1, P[e + "upsample_latent1.0"], self.t96_256b, M=96 * 96, N=256, K=D)
@@ -582,7 +589,8 @@ class Engine:
             # projections need their outputs (enc3, enc2, enc1; enc0 last).  Side streams issue no
             # stream-K launch that could overlap one of the main stream's (workgroups that wait on
             # each other, dp_mi355x.h): no workspace here.
-            for st, chains in ((self.dec_a, (("enc0", lat0_chain),)),
+            lat0_sk = self.lat0_sk
+            for st, chains in ((self.dec_a, (("enc0pre", lat0_pre) if lat0_sk else ("enc0", lat0_chain),)),
                                (self.dec_b, (("enc3", f1_chain), ("enc2", f0_chain), ("enc1", lat1_chain)))):
                 st.wait_stream(main)
                 with torch.cuda.stream(st), ops.use_workspace(None):
@@ -622,6 +630,14 @@ class Engine:
                     self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256)
                     evs[i] = torch.cuda.Event()
                     evs[i].record(self.dec_c)
+                # the lat0 chain's last deconv (on stream-K: 164 vs 446 us data-parallel) here, on the
+                # stream-K side stream; the main stream waits for it before fusion 1, whose deconv
+                # is its next stream-K launch
+                if lat0_sk:
+                    self.dec_c.wait_event(enc_ev["enc0pre"])
+                    lat0_last()
+                    enc_ev["enc0"] = torch.cuda.Event()
+                    enc_ev["enc0"].record(self.dec_c)
         elif self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
             if self.side_streams == 2 and not serial:
                 main.wait_stream(self.side2)
@@ -638,6 +654,8 @@ class Engine:
                 c = self.dec[s]["c"]
                 if par:
                     main.wait_event(evs[i])
+                    if i == 1:
+                        main.wait_event(enc_ev["enc0"])
                 else:
                     self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
                 f = self._fusion(i, f, s, c)
