@@ -142,6 +142,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct resident frames per rank")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="1: frame pipeline (depth_pro.pipeline: frame i+1's image/FOV encoders beside frame i's "
+                         "decoder, two engines; measured slower, DESIGN.md 7); 0: one DepthPro.infer-style "
+                         "engine, frame by frame (default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,9 +173,14 @@ def main():
         packed = D.broadcast_packed(packed, dev, src=0)
     else:
         packed = pack_weights(synthetic_state_dict(0), dev, code)
-    eng = Engine(packed, dev, code)
-    if not args.no_graph:
-        eng.capture_graph()
+    if args.pipeline:
+        from depth_pro.pipeline import FramePipeline, u8_loader
+        pipe = FramePipeline(packed, dev, code, graph=not args.no_graph)
+        eng = pipe.E[0]
+    else:
+        eng = Engine(packed, dev, code)
+        if not args.no_graph:
+            eng.capture_graph()
     torch.cuda.synchronize()
     t_setup = time.time() - t_setup
 
@@ -184,13 +193,22 @@ def main():
     fpx = torch.empty((), dtype=torch.float32, device=dev)
     pending = [None, None]
 
+    if args.pipeline:
+        loaders = [u8_loader(f) for f in frames]
+    counter = [0]
+
     def step(i):
         d = depths[i & 1]
         if pending[i & 1] is not None:
             pending[i & 1].wait()
             pending[i & 1] = None
-        ops.normalize_u8(frames[i % len(frames)], eng.x0)
-        c, fov = eng.run()
+        n = counter[0]
+        counter[0] += 1
+        if args.pipeline:    # frame n's patch encoder + decoder, frame n+1's side encoders beside them
+            c, fov = pipe.step(loaders[n % len(frames)], loaders[(n + 1) % len(frames)])
+        else:
+            ops.normalize_u8(frames[n % len(frames)], eng.x0)
+            c, fov = eng.run()
         ops.infer_epilogue(c, fov, None, 1536, 1536, d, fpx)
         if world > 1:
             _, pending[i & 1] = D.gather_frames(d, dst=0, async_op=True)
@@ -246,11 +264,17 @@ def main():
 
     parity = None
     if rank == 0:
-        ops.normalize_u8(frames[0], eng.x0)          # rank 0 holds frame 0 of the stream
-        c, fov = eng.run()
+        if args.pipeline:    # a fresh two-frame stream starting at frame 0 (rank 0 holds frame 0)
+            pipe.primed = False
+            c, fov = pipe.step(loaders[0], loaders[1 % len(frames)])
+        else:
+            ops.normalize_u8(frames[0], eng.x0)
+            c, fov = eng.run()
         ops.infer_epilogue(c, fov, None, 1536, 1536, depth, fpx)
         torch.cuda.synchronize()
         parity = depth_parity(depth, c, fov)
+        if args.pipeline:
+            pipe.check_status()
 
     if rank == 0:
         achieved = fps_per_gpu * FLOP_PER_FRAME / 1e12
@@ -296,8 +320,13 @@ def main():
             "dtype": {"bf16": "bf16", "fp16": "f16", "mixed": "bf16+f16"}[args.dtype],
             "data": "synthetic (uint8 1536x1536 frames from numpy default_rng(k); synthetic seed-0 weights, "
                     "full Depth Pro architecture, 951,991,330 params)",
-            "config": {"workload": "BASELINE config 2/3: one 1536x1536 frame per GPU per step through "
-                                   "DepthPro.infer (patch+image+FOV ViT-L, decoder, heads), hipGraph replay",
+            "config": {"workload": ("BASELINE config 3: steady-state 1536x1536 video stream, one frame per GPU "
+                                    "per step (patch+image+FOV ViT-L, decoder, heads, infer epilogue), frame "
+                                    "pipeline: frame i+1's image/FOV encoders beside frame i's decoder, hipGraph "
+                                    "replay of each phase") if args.pipeline else
+                                   ("BASELINE config 2/3: one 1536x1536 frame per GPU per step through "
+                                    "DepthPro.infer (patch+image+FOV ViT-L, decoder, heads), hipGraph replay"),
+                       "pipeline": bool(args.pipeline),
                        "global_batch": world, "frame": [1536, 1536], "parallelism": f"frame-dp{world}",
                        "graph": not args.no_graph,
                        "precision": {"bf16": "bf16 everywhere", "fp16": "f16 everywhere",

@@ -486,12 +486,18 @@ class Engine:
         self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
         ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
 
-    def forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Run the network on `self.x0`; results in self.canonical / self.fov_deg."""
-        with ops.use_workspace(self.ws_main):
-            return self._forward()
+    def forward(self, phase: str = "all") -> Tuple[torch.Tensor, torch.Tensor]:
+        """Run the network on `self.x0`; results in self.canonical / self.fov_deg.
 
-    def _forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        `phase` splits the forward for the frame pipeline (depth_pro.pipeline): "side" = window
+        im2col + the image and FOV encoders, "enc" = the patch encoder, "dec" = everything after
+        it; the caller orders them (side before dec, enc before dec).  "all" = the whole frame."""
+        if phase not in ("all", "side", "enc", "dec"):
+            raise DPError(f"unknown forward phase {phase!r}")
+        with ops.use_workspace(self.ws_main):
+            return self._forward(phase)
+
+    def _forward(self, phase: str = "all") -> Tuple[torch.Tensor, torch.Tensor]:
         """Body of `forward`.
 
         Two streams: the current stream runs the patch encoder -> decoder -> head;
@@ -504,9 +510,22 @@ class Engine:
         P = self.P
         main = torch.cuda.current_stream(self.dev)
         side_ok = "side" not in _ABLATE
-        ops.patchify_pyramid(self.x0, self.cols)
         serial = self.serial_side or self.side_mode == "serial"
         fov_side = self.use_fov and self.fov_late and not serial
+        if phase != "all" and (serial or fov_side or self.side_mode != "concurrent" or len(self.patch_groups) != 1):
+            raise DPError("forward phases need the default schedule (concurrent side encoders, one window group)")
+        if phase in ("all", "side"):
+            ops.patchify_pyramid(self.x0, self.cols)
+        if phase == "side":
+            # the image encoder on this stream, the FOV encoder on side2, joined before returning
+            with ops.use_workspace(self.ws_side):
+                self._image_encoder()
+            if self.use_fov:
+                self.side2.wait_stream(main)
+                with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
+                    self._fov_encoder()
+                main.wait_stream(self.side2)
+            return self.canonical, self.fov_deg
 
         def side_encoders():
             if serial:
@@ -534,10 +553,12 @@ class Engine:
         # image encoder (it is needed only at the FOV head, after the decoder's first conv)
         fov_at = self.fov_at if (self.use_fov and not fov_side and self.side_streams == 2 and not serial
                                  and len(self.patch_groups) == 1) else -1
-        if self.side_mode != "late" or serial:
+        if phase == "all" and (self.side_mode != "late" or serial):
             side_encoders()
         vp = self.vp
-        if len(self.patch_groups) == 1:
+        if phase == "dec":
+            pass
+        elif len(self.patch_groups) == 1:
             hooks = {
                 5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
                 11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
@@ -548,9 +569,12 @@ class Engine:
             self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True)
         else:
             self._patch_groups(main)
-        ops.merge_windows(vp.out, 0, 5, 3, self.f0)
-        ops.merge_windows(vp.out, 25, 3, 6, self.f1)
-        ops.merge_windows(vp.out, 34, 1, 0, self.f2)
+        if phase != "dec":
+            ops.merge_windows(vp.out, 0, 5, 3, self.f0)
+            ops.merge_windows(vp.out, 25, 3, 6, self.f1)
+            ops.merge_windows(vp.out, 34, 1, 0, self.f2)
+        if phase == "enc":
+            return self.canonical, self.fov_deg
         if self.side_mode == "late" and not serial:
             side_encoders()
         # project / upsample (encoder.py:314-324)
@@ -605,7 +629,7 @@ class Engine:
             f1_chain()
         ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
-        if not serial:
+        if not serial and phase == "all":
             main.wait_stream(self.side)  # join: image-encoder half of `cat` and fov tokens ready
         ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
@@ -639,7 +663,7 @@ class Engine:
                     enc_ev["enc0"] = torch.cuda.Event()
                     enc_ev["enc0"].record(self.dec_c)
         elif self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
-            if self.side_streams == 2 and not serial:
+            if self.side_streams == 2 and not serial and phase == "all":
                 main.wait_stream(self.side2)
             self._fov_head()
         elif fov_side:

@@ -293,3 +293,34 @@ def test_forward_fused_layernorm_vs_reference(model, golden_dir):
         assert e_c < m.tol["canon"] and e_f < m.tol["fov"]
     finally:
         e.ln_fuse, e.graph = f0, graph
+
+
+def test_frame_pipeline_matches_single_frame(model):
+    """depth_pro.pipeline.FramePipeline (two engines, frame i+1's image/FOV encoders beside frame
+    i's decoder, captured side / enc / dec phases) gives every frame of a 4-frame stream bit for
+    bit the outputs of the single-frame engine."""
+    m, _ = model
+    if m.tag != "mixed":
+        pytest.skip("one precision mode is enough for the schedule")
+    from depth_pro import ops
+    from depth_pro.pipeline import FramePipeline, u8_loader
+
+    e = m.engine()
+    dev = e.dev
+    frames = [torch.from_numpy(frame(20 + k)).to(dev) for k in range(4)]
+    ref = []
+    for f in frames:
+        ops.normalize_u8(f, e.x0)
+        c, fov = e.run()
+        ref.append((c.clone(), fov.clone()))
+    pipe = FramePipeline(e.P, dev, m.compute_dtype)
+    loaders = [u8_loader(f) for f in frames]
+    got = []
+    for c, fov in pipe.run(loaders):
+        got.append((c.clone(), fov.clone()))
+    torch.cuda.synchronize()
+    pipe.check_status()
+    for k, ((c0, f0), (c1, f1)) in enumerate(zip(ref, got)):
+        assert torch.equal(c0, c1) and torch.equal(f0, f1), f"frame {k}: max|d| {(c0 - c1).abs().max().item():.3e}"
+    del pipe
+    torch.cuda.empty_cache()
