@@ -78,10 +78,13 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
 // isomorphic for the compiler to SLP-pack into v_pk_add_f32, which costs more issue beside
 // MFMAs).  Not inline asm: an asm add that reads a v_exp_f32 result right away misses the
 // transcendental-use wait state the compiler inserts for its own instructions.
-template <typename K_, bool LAZY, bool VSUM, bool PF, bool PRE = false, bool SADD = false>
-__global__ void __launch_bounds__(256, PF ? 3 : 4)
+// NST: K/V ring depth.  3 = tile t+2's LDS-DMA issued at the top of tile t (two tiles of
+// compute cover each load; 48 KiB per workgroup: 3 workgroups per CU instead of 4).
+template <typename K_, bool LAZY, bool VSUM, bool PF, bool PRE = false, bool SADD = false, int NST = 2>
+__global__ void __launch_bounds__(256, (PF || NST == 3) ? 3 : 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
-  __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
+  __shared__ __attribute__((aligned(1024))) char smem[NST][2 * TILE_B];   // [stage][K tile | V tile]
+  auto stage_of = [](int t) { return NST == 2 ? (t & 1) : (t % NST); };
   __shared__ int redo;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -173,7 +176,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   // `exact` is a workgroup-uniform runtime flag, so the redo pass reuses this code.
   auto do_half = [&](int t, int kb, auto partial_tag, bool setmax, bool exact) __attribute__((always_inline)) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
-    const int cur = t & 1;
+    const int cur = stage_of(t);
     const int kbase = t * KT;
     const char* K = smem[cur];
     const char* V = smem[cur] + TILE_B;
@@ -250,12 +253,12 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   };
   // ---- PF variant of a half tile, in stages
   auto read_k = [&](int t, int kb, uint4 (&kf)[4]) __attribute__((always_inline)) {
-    const char* K = smem[t & 1];
+    const char* K = smem[stage_of(t)];
     #pragma unroll
     for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
   };
   auto read_v = [&](int t, int kb, uint4 (&vf)[2][2]) __attribute__((always_inline)) {
-    const char* V = smem[t & 1] + TILE_B;
+    const char* V = smem[stage_of(t)] + TILE_B;
     #pragma unroll
     for (int st = 0; st < 2; ++st)
       #pragma unroll
@@ -397,18 +400,31 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     for (int i = 0; i < 4; ++i) ls4[i] = 0.f;
     m_run = -INFINITY;
     if (nmma > 0) issue(0, 0);
+    if constexpr (NST == 3) {
+      if (nmma > 1) issue(KT, 1);
+    }
+    // top of tile t: tile t landed (own pieces: counted vmcnt -- each issue is 4 pieces per
+    // thread; everyone's: the barrier, which also frees the stage of tile t-1 for the next issue)
+    auto top = [&](int t) __attribute__((always_inline)) {
+      if constexpr (NST == 3) {
+        if (t + 1 < nmma) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (t + 2 < nmma) issue((t + 2) * KT, stage_of(t + 2));
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (t + 1 < nmma) issue((t + 1) * KT, stage_of(t + 1));
+      }
+    };
     if (nfull > 0) {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      if (1 < nmma) issue(KT, 1);
+      top(0);
       do_tile(0, std::false_type{}, true, exact);
     }
     for (int t = 1; t < nfull; ++t) {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      if (t + 1 < nmma) issue((t + 1) * KT, (t + 1) & 1);
+      top(t);
       do_tile(t, std::false_type{}, false, exact);
     }
     if (nfull < nmma) {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      top(nfull);
       do_tile(nfull, std::true_type{}, nfull == 0, exact);
     }
     if (valu_tail && active) {
@@ -498,7 +514,12 @@ int attention_launch(const void* qkv, void* out, int32_t batch, int32_t seq, int
   } while (0)
   // DP_ATTN_SADD=0: packed row-sum adds in the log2q kernel (A/B)
   static const bool sadd = [] { const char* e = getenv("DP_ATTN_SADD"); return !(e && e[0] == '0'); }();
-  if (pre) {   // the default kernel (lazy max, VALU row sums) with log2-unit Q
+  // DP_ATTN_NST=3: 3-deep K/V ring in the log2q kernel (A/B)
+  static const bool nst3 = [] { const char* e = getenv("DP_ATTN_NST"); return e && e[0] == '3'; }();
+  if (pre && sadd && nst3) {
+    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true, true, 3>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true, true, 3>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+  } else if (pre) {   // the default kernel (lazy max, VALU row sums) with log2-unit Q
     if (sadd) {
       if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
       else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
