@@ -295,6 +295,7 @@ class Engine:
         self.ws_dec = ops.gemm_workspace(dev)
         self.dec_streams = os.environ.get("DP_DEC_STREAMS", "1") == "1"
         self.small_conv_tile = int(os.environ.get("DP_SMALL_CONV_TILE", "0"))
+        self.conv768_tile = int(os.environ.get("DP_CONV768_TILE", "0"))
         self.fov_at = int(os.environ.get("DP_FOV_AT", "-1"))
         self.lat0_sk = os.environ.get("DP_LAT0_SK", "1") == "1"
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
@@ -395,6 +396,9 @@ class Engine:
         # A/B (DP_SMALL_CONV_TILE, a DP_TILE_* value): engine of the decoder's small-grid
         # ResidualBlock convs (48^2 / 96^2: 9 / 36 tiles of 256 x 256 on 256 CUs)
         tile = self.small_conv_tile if (self.small_conv_tile and s_out <= 96 and cout == 256 and cin == 256) else 0
+        # A/B (DP_CONV768_TILE): engine of the 768^2 ResidualBlock convs (default: persistent 256 x 256)
+        if self.conv768_tile and s_out == 768 and cout == 256 and cin == 256:
+            tile = self.conv768_tile
         ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
                  conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
                  relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout,
