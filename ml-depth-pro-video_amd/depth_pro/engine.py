@@ -296,6 +296,7 @@ class Engine:
         self.dec_streams = os.environ.get("DP_DEC_STREAMS", "1") == "1"
         self.small_conv_tile = int(os.environ.get("DP_SMALL_CONV_TILE", "0"))
         self.conv768_tile = int(os.environ.get("DP_CONV768_TILE", "0"))
+        self.qkv_tile = int(os.environ.get("DP_QKV_TILE", "0"))   # A/B: patch-encoder qkv engine
         self.fov_at = int(os.environ.get("DP_FOV_AT", "-1"))
         self.lat0_sk = os.environ.get("DP_LAT0_SK", "1") == "1"
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
@@ -365,7 +366,7 @@ class Engine:
                 ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"],
-                         gamma=self.qkv_gamma, tile=t)
+                         gamma=self.qkv_gamma, tile=t or (self.qkv_tile if n_img > 1 else 0))
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=self.qkv_gamma is not None)
             ln2 = (P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, 1e-6) if fuse else None
