@@ -324,3 +324,26 @@ def test_frame_pipeline_matches_single_frame(model):
         assert torch.equal(c0, c1) and torch.equal(f0, f1), f"frame {k}: max|d| {(c0 - c1).abs().max().item():.3e}"
     del pipe
     torch.cuda.empty_cache()
+
+
+def test_decoder_streams_match_serial_schedule(model):
+    """The post-encoder schedule on four streams (Engine.dec_streams: upsample chains, FOV head and
+    the decoder's projections beside the main stream) gives bit for bit the outputs of the serial
+    order: the same kernels on the same data, only their placement differs."""
+    m, transform = model
+    if m.tag != "mixed":
+        pytest.skip("one precision mode is enough for the schedule")
+    e = m.engine()
+    x = transform(frame(7)).unsqueeze(0)
+    d0, graph = e.dec_streams, e.graph
+    try:
+        e.graph = None
+        e.dec_streams = False
+        c1, f1 = (t.clone() for t in m.forward(x))
+        e.dec_streams = True
+        c2, f2 = m.forward(x)
+        torch.cuda.synchronize()
+        e.check_status(block=True)
+        assert torch.equal(c1, c2) and torch.equal(f1, f2), (c1 - c2).abs().max().item()
+    finally:
+        e.dec_streams, e.graph = d0, graph
