@@ -297,6 +297,7 @@ class Engine:
         self.small_conv_tile = int(os.environ.get("DP_SMALL_CONV_TILE", "0"))
         self.conv768_tile = int(os.environ.get("DP_CONV768_TILE", "0"))
         self.qkv_tile = int(os.environ.get("DP_QKV_TILE", "0"))   # A/B: patch-encoder qkv engine
+        self.side_sync = os.environ.get("DP_SIDE_SYNC", "0") == "1"
         self.fov_at = int(os.environ.get("DP_FOV_AT", "-1"))
         self.lat0_sk = os.environ.get("DP_LAT0_SK", "1") == "1"
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
@@ -343,7 +344,15 @@ class Engine:
             raise DPError(f"DP_SIDE_MODE={self.side_mode!r}")
 
     # ------------------------------------------------------------------ ViT
-    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, ln_fuse=False):
+    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, ln_fuse=False,
+             pre_fc1=None, pre_fc2=None):
+        for _ in self._vit_iter(pre, buf, n_img, cols_off_rows, hooks, ln_fuse, pre_fc1, pre_fc2):
+            pass
+
+    def _vit_iter(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, ln_fuse=False,
+                  pre_fc1=None, pre_fc2=None):
+        """The ViT as a generator: yields after each block (the side encoders step block by block
+        beside the patch encoder, DP_SIDE_SYNC); pre_fc1 / pre_fc2: callbacks before those GEMMs."""
         P, M = self.P, n_img * TOK
         # side encoders (one image, M = 577): engine choice for CU-time, not latency (DP_SIDE_TILE)
         t = self.side_tile if n_img == 1 else 0
@@ -380,13 +389,19 @@ class Engine:
             if fuse:
                 ln1 = ((P[nb + "norm1.weight"], P[nb + "norm1.bias"], buf.h, 1e-6) if i + 1 < DEPTH else
                        (P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, 1e-6))
+            if pre_fc1:
+                pre_fc1(i)
             if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
                          act=DP_ACT_GELU, tile=t)
+            if pre_fc2:
+                pre_fc2(i)
+            if "vitgemm" not in _ABLATE:
                 ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
                          gamma=P[b + "ls2.gamma"], accumulate=True, tile=t, ln=ln1)
             if hooks and i in hooks:
                 hooks[i]()
+            yield i
         if not fuse:
             ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
 
@@ -466,6 +481,19 @@ class Engine:
                 main.wait_stream(st)
 
     # -------------------------------------------------------------- forward
+    def _image_encoder_iter(self):
+        """_image_encoder as a generator (one step per ViT block, the tail after the last)."""
+        P, e = self.P, "encoder."
+        yield from self._vit_iter("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
+        ops.merge_windows(self.vi.out, 0, 1, 0, self.g)
+        self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
+                     C_off=D, ldc=2 * D)
+
+    def _fov_encoder_iter(self):
+        vf, P = self.vf, self.P
+        yield from self._vit_iter("fov.encoder.0.", vf, 1, 34 * PTOK)
+        ops.gemm(vf.out, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
+
     def _image_encoder(self):
         """Image encoder (+ lowres upsample): ~2.5 % of the frame's FLOPs at M = 577
         rows, far too few tiles to fill 256 CUs alone, so it runs on a side stream
@@ -558,7 +586,26 @@ class Engine:
         # image encoder (it is needed only at the FOV head, after the decoder's first conv)
         fov_at = self.fov_at if (self.use_fov and not fov_side and self.side_streams == 2 and not serial
                                  and len(self.patch_groups) == 1) else -1
-        if phase == "all" and (self.side_mode != "late" or serial):
+        # DP_SIDE_SYNC (A/B): the side encoders step one block per patch-encoder block, each step
+        # beside that block's fc1 (multi-round, its last round leaves CUs free) and joined before
+        # its fc2, so they never hold CUs when a one-round proj / fc2 launches
+        sync = (self.side_sync and phase == "all" and not serial and not fov_side and self.side_mode == "concurrent"
+                and self.side_streams == 2 and self.use_fov and side_ok and fov_at < 0 and len(self.patch_groups) == 1)
+        side_its = None
+        if sync:
+            side_its = [(self.side, self.ws_side, self._image_encoder_iter()),
+                        (self.side2, self.ws_side2, self._fov_encoder_iter())]
+
+            def side_step(i):
+                for st, ws, it in side_its:
+                    st.wait_stream(main)
+                    with torch.cuda.stream(st), ops.use_workspace(ws):
+                        next(it)
+
+            def side_join(i):
+                main.wait_stream(self.side)
+                main.wait_stream(self.side2)
+        elif phase == "all" and (self.side_mode != "late" or serial):
             side_encoders()
         vp = self.vp
         if phase == "dec":
@@ -571,7 +618,15 @@ class Engine:
             if fov_at >= 0:
                 prev = hooks.get(fov_at)
                 hooks[fov_at] = (lambda: (prev(), fov_encoder_side2())) if prev else fov_encoder_side2
-            self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True)
+            if sync:
+                self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True, pre_fc1=side_step,
+                          pre_fc2=side_join)
+                for st, ws, it in side_its:          # the side encoders' final norm and tails
+                    with torch.cuda.stream(st), ops.use_workspace(ws):
+                        for _ in it:
+                            pass
+            else:
+                self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True)
         else:
             self._patch_groups(main)
         if phase != "dec":

@@ -1,2 +1,2 @@
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && O=gpurun_out/r02z10 && mkdir -p $O && \
-timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py -x -v --timeout 300 --timeout-method thread -k "decoder_streams or pipeline or graph_replays" > $O/t_model.log 2>&1
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && O=gpurun_out/r02z11 && mkdir -p $O && \
+for S in 1 0 1 0; do DP_SIDE_SYNC=$S timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $O/b.json 2> $O/b.err || exit 1; echo "{\"sync\": $S, \"r\": $(cat $O/b.json)}" >> $O/all.jsonl; done
