@@ -111,7 +111,11 @@ typedef struct dp_gemm_args {
   int32_t row_group, row_group_out, row_off;
   const float* head_w;      /* [N] or NULL */
   float head_b;
-  const float* head_corr;   /* DP_STORE_HEAD_PS: [9][32] border corrections, else NULL */
+  const float* head_corr;   /* DP_STORE_HEAD_PS: [9][32] border corrections; DP_STORE_ROWS with a
+                               stride-1 pad-1 3x3 implicit conv on the 512x128 engine (N = 128 at
+                               M >= 512*256, or that tile hint): [9][N] per-tap values
+                               subtracted where the tap falls in the zero padding (a composed
+                               1x1-then-3x3 conv's bias); else NULL */
   int32_t tile;             /* 0 = auto, else a DP_TILE_* hint */
   void* workspace;          /* NULL, or >= dp_gemm_workspace_size() bytes of device memory owned by
                                the caller for THIS stream (never shared by concurrent launches);

@@ -325,11 +325,36 @@ __device__ __forceinline__ void add8_u4(float (&v)[8], uint4 r) {
     v[2 * k + 1] += K_::to_f(w[k] >> 16);
   }
 }
+// Composed 3x3-after-1x1 conv (DP_STORE_ROWS with head_corr, engine.compose_head0): the 1x1's
+// bias rides in the composed bias for all 9 taps; at the image border the taps that fall in
+// the 3x3's zero padding must not contribute it: subtract corr[(ky*3+kx)*N + n] for each.
+__device__ __forceinline__ void border_correct(const GemmP& p, int m, int nc, float (&z)[8]) {
+  const int hw = p.out_h * p.out_w;
+  const int rr = m % hw;
+  const int yy = rr / p.out_w, xx = rr - yy * p.out_w;
+  const bool top = yy == 0, bot = yy == p.out_h - 1, lft = xx == 0, rgt = xx == p.out_w - 1;
+  if (!(top || bot || lft || rgt)) return;
+  // a rolled loop with two 16-B loads per tap: few live registers in an epilogue that is
+  // already at the 256-VGPR limit (the unrolled 9 x 8 form cost 71 spills)
+  #pragma unroll 1
+  for (int t = 0; t < 9; ++t) {
+    const int a = t / 3, c = t - 3 * (t / 3);
+    const bool oob = (a == 0 && top) || (a == 2 && bot) || (c == 0 && lft) || (c == 2 && rgt);
+    if (oob) {
+      const float4 lo = *(const float4*)(p.head_corr + t * p.N + nc);
+      const float4 hi = *(const float4*)(p.head_corr + t * p.N + nc + 4);
+      z[0] -= lo.x; z[1] -= lo.y; z[2] -= lo.z; z[3] -= lo.w;
+      z[4] -= hi.x; z[5] -= hi.y; z[6] -= hi.z; z[7] -= hi.w;
+    }
+  }
+}
 // v[it][0..7] = accumulators of row ms[it], columns n..n+7.  Loads go to clamped
 // (always valid) rows with no predicate, so the compiler issues the whole batch
 // back to back instead of sinking each load into its own branch; only the
 // stores are predicated.
-template <typename K_, int NIT>
+// BC: this instantiation applies the composed-conv border correction (only the 512 x 128 conv
+// engine has it: compiled into every engine's epilogue it costs the 320 x 256 one ~170 spills)
+template <typename K_, int NIT, bool BC = false>
 __device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc, const int (&ms)[NIT], int n,
                                               float (&v)[NIT][8]) {
   const int nc = n < p.N ? n : p.N - 8;
@@ -364,6 +389,9 @@ __device__ __forceinline__ void epilogue_rows(const GemmP& p, const ColConst& cc
     float (&x)[8] = v[it];
     #pragma unroll
     for (int r = 0; r < 8; ++r) x[r] += cc.b[r];
+    if constexpr (BC) {
+      if (p.head_corr) border_correct(p, mc[it], nc, x);
+    }
     if (p.act == DP_ACT_RELU) {
       #pragma unroll
       for (int r = 0; r < 8; ++r) x[r] = fmaxf(x[r], 0.f);
@@ -923,7 +951,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
           continue;
         }
       }
-      epilogue_rows<K_, NITC>(p, cc, ms, n_l, v);
+      epilogue_rows<K_, NITC, CONV && BM == 512 && !RELU>(p, cc, ms, n_l, v);
       if constexpr (LNF) {
         // the new rows stay in the registers of the accumulators this pass consumed
         // (8 * FN floats per lane per pass, same count), and each wave publishes, per row,
@@ -2090,6 +2118,13 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
         a->accumulate || a->R1 || a->R2 || a->pos || a->gamma || a->act != DP_ACT_NONE)
       return DP_ERR_ARG;
   }
+  if (a->store_mode == DP_STORE_ROWS && a->head_corr) {
+    // composed conv with border correction: a stride-1, pad-1 3x3 implicit conv, rows = pixels
+    if (a->a_mode != DP_A_CONV || a->k_h != 3 || a->k_w != 3 || a->pad != 1 || a->stride != 1 || a->head_w ||
+        a->row_group || a->out_h != a->in_h || a->out_w != a->in_w || a->N % 8 != 0 || a->N < 128 ||
+        (a->tile != DP_TILE_AUTO && a->tile <= DP_TILE_256x32))   // the small engines have no correction
+      return DP_ERR_ARG;
+  }
   if (a->store_mode == DP_STORE_DECONV2X2) {
     if (a->dc_cout % 4 != 0 || a->N != 4 * a->dc_cout || a->dc_h <= 0 || a->dc_w <= 0 ||
         a->M % (a->dc_h * a->dc_w) != 0)
@@ -2158,7 +2193,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   // byte extent of C for the persistent engine's bounded buffer stores (0: not eligible)
   unsigned c_bytes = 0;
-  if (a->store_mode == DP_STORE_ROWS && !a->head_w) {
+  if (a->store_mode == DP_STORE_ROWS && !a->head_w && !a->head_corr) {
     long long last = a->M - 1;
     if (a->row_group) last = (last / a->row_group) * a->row_group_out + a->row_off + last % a->row_group;
     const long long ext = (last * a->ldc + a->N) * (a->c_dtype == DP_F32 ? 4 : 2);
@@ -2190,6 +2225,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       tile = DP_TILE_PBIG_256x256;
   }
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
+  // the border-corrected composed conv exists in the 512 x 128 conv engine only
+  if (a->store_mode == DP_STORE_ROWS && a->head_corr && tile != DP_TILE_BIG_512x128) return DP_ERR_ARG;
 
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;

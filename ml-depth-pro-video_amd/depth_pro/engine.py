@@ -85,6 +85,23 @@ def compose_head(wd: torch.Tensor, bd: torch.Tensor, w2: torch.Tensor, b2: torch
             "head.ps.corr": corr.reshape(-1).contiguous()}
 
 
+def compose_head0(w0: torch.Tensor, b0: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, dt) -> Dict[str, object]:
+    """Compose the decoder's last 1x1 `out_conv` (decoder.fusions.0.out_conv, decoder.py:184) with
+    the head's first 3x3 conv (head.0, depth_pro.py:182-207) -- linear, nothing in between -- into
+    ONE 3x3 conv over the fusion block's output:
+
+        W'[o, c, ky, kx] = sum_m W0[o, m, ky, kx] Wo[m, c],   corr[ky, kx, o] = sum_m W0[o, m, ky, kx] bo[m]
+
+    with bias b0 + sum over the 9 taps of corr; a tap that falls in head.0's zero padding must not
+    contribute its corr (the 1x1's output is 0 there, not bo): the GEMM epilogue subtracts it at
+    the image border (DP_STORE_ROWS with head_corr).  Removes the 768^2 x 256 1x1 GEMM and its
+    302 MB map from the frame."""
+    wc = torch.einsum("omyx,mc->ocyx", w0, wo)
+    corr = torch.einsum("omyx,m->yxo", w0, bo).contiguous()          # [3, 3, o]
+    bias = (b0 + corr.sum(dim=(0, 1))).contiguous()
+    return {"head.0c.w": ops.conv_weight(wc, dt), "head.0c.b": bias, "head.0c.corr": corr.reshape(-1).contiguous()}
+
+
 def precision_codes(codes) -> Tuple[int, int]:
     """(ViT code, decoder code) from one DP_BF16 / DP_F16 code or a pair of them.
 
@@ -168,6 +185,9 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code) 
     # head
     P["head.0.w"] = _conv_w(g("head.0.weight"), dt)
     P["head.0.b"] = _f32(g("head.0.bias"))
+    P.update(compose_head0(_f32(g("head.0.weight")), _f32(g("head.0.bias")),
+                           _f32(g("decoder.fusions.0.out_conv.weight"))[:, :, 0, 0],
+                           _f32(g("decoder.fusions.0.out_conv.bias")), dt))
     P.update(compose_head(_f32(g("head.1.weight")), _f32(g("head.1.bias")), _f32(g("head.2.weight")),
                           _f32(g("head.2.bias")), dt))
     P["head.4.w"] = _f32(g("head.4.weight")).reshape(-1)
@@ -298,6 +318,8 @@ class Engine:
         self.conv768_tile = int(os.environ.get("DP_CONV768_TILE", "0"))
         self.qkv_tile = int(os.environ.get("DP_QKV_TILE", "0"))   # A/B: patch-encoder qkv engine
         self.side_sync = os.environ.get("DP_SIDE_SYNC", "0") == "1"
+        # decoder out_conv composed into the head's first conv (compose_head0); DP_HEAD0_COMPOSE=0: separate
+        self.head0_compose = os.environ.get("DP_HEAD0_COMPOSE", "1") == "1" and "head.0c.w" in packed
         self.fov_at = int(os.environ.get("DP_FOV_AT", "-1"))
         self.lat0_sk = os.environ.get("DP_LAT0_SK", "1") == "1"
         # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
@@ -407,7 +429,7 @@ class Engine:
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
-               stride=1, head_w=None, head_b=0.0):
+               stride=1, head_w=None, head_b=0.0, border_corr=None):
         s_out = (s_in + 2 - 3) // stride + 1
         # A/B (DP_SMALL_CONV_TILE, a DP_TILE_* value): engine of the decoder's small-grid
         # ResidualBlock convs (48^2 / 96^2: 9 / 36 tiles of 256 x 256 on 256 CUs)
@@ -418,7 +440,7 @@ class Engine:
         ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
                  conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
                  relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout,
-                 head_w=head_w, head_b=head_b, ldc=cout, tile=tile)
+                 head_w=head_w, head_b=head_b, ldc=cout, tile=tile, border_corr=border_corr)
 
     def _deconv(self, x, s_in, cin, w, out, cout, bias=None, C_off=0, ldc=None):
         ops.gemm(x, w, out, M=s_in * s_in, N=4 * cout, K=cin, bias=bias, deconv=(s_in, s_in, cout),
@@ -444,6 +466,8 @@ class Engine:
             out = self.up[2 * s]
             self._deconv(d["y"], s, 256, P[p + "up.w"], out, 256, bias=P[p + "up.b"])
             return out
+        if self.head0_compose:   # out_conv is composed into head.0 (compose_head0)
+            return d["y"]
         ops.gemm(d["y"], P[p + "out.w"], self.feats, M=s * s, N=256, K=256, bias=P[p + "out.b"])
         return self.feats
 
@@ -760,7 +784,11 @@ class Engine:
             return self.canonical, self.fov_deg
         # head (depth_pro.py:182-207): conv3x3, then deconv -> conv3x3 -> ReLU -> 1x1 -> ReLU as ONE
         # composed 3x3 conv over h0 with a pixel-shuffle + fused 1x1 epilogue (compose_head)
-        self._conv3(feats, 768, 256, P["head.0.w"], self.h0, 128, bias=P["head.0.b"])
+        if self.head0_compose and "decoder" not in _ABLATE:
+            self._conv3(feats, 768, 256, P["head.0c.w"], self.h0, 128, bias=P["head.0c.b"],
+                        border_corr=P["head.0c.corr"])
+        else:
+            self._conv3(feats, 768, 256, P["head.0.w"], self.h0, 128, bias=P["head.0.b"])
         ops.gemm(self.h0, P["head.ps.w"], self.canonical, M=768 * 768, N=128, K=9 * 128,
                  conv=dict(in_h=768, in_w=768, in_c=128, k=3, stride=1, pad=1, out_h=768, out_w=768),
                  bias=P["head.ps.b"], head_w=P["head.4.w"], head_b=P["head.4.b"], head_corr=P["head.ps.corr"])

@@ -135,7 +135,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          head_corr: Optional[torch.Tensor] = None,
          A_off: int = 0, C_off: int = 0, B_off: int = 0, tile: int = 0,
          workspace: Optional[torch.Tensor] = None,
-         plan_only: bool = False, ln: Optional[tuple] = None):
+         plan_only: bool = False, ln: Optional[tuple] = None, border_corr: Optional[torch.Tensor] = None):
     """dp_gemm. `A_off`/`B_off`/`C_off` are element offsets into A / B / C (sub-views, e.g. a
     K slice of a split-K GEMM: A_off = B_off = k0 with lda / ldb the full row lengths).
 
@@ -182,7 +182,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     a.row_group, a.row_group_out, a.row_off = row_group, row_group_out, row_off
     a.head_w = _p(head_w)
     a.head_b = float(head_b)
-    a.head_corr = _p(head_corr)
+    if border_corr is not None and border_corr.numel() < 9 * N:
+        raise _lib.DPError("dp_gemm: border_corr needs 9 * N values")
+    a.head_corr = _p(head_corr if head_corr is not None else border_corr)
     a.tile = tile
     ws = workspace if workspace is not None else _WS
     if ws is not None:

@@ -606,3 +606,28 @@ def test_gemm_residual_layernorm(cuda, case):
             assert torch.equal(C, ref)
             assert bool(((y.float() - lref).abs() <= lref.abs() * 2.0 ** -8 + 1e-4).all())
             assert int(cnt.abs().sum()) == 0 and ops.workspace_error(ws) == 0
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_conv3x3_border_corrected_composition(cuda, dt):
+    """dp_gemm DP_STORE_ROWS with head_corr (the decoder out_conv composed into head.0,
+    engine.compose_head0): equals the reference 1x1 conv then zero-padded 3x3 conv in fp32, at
+    96 x 96 x 256 -> 128 (the 768^2 shape's engine family), every border pixel included."""
+    from depth_pro.engine import compose_head0
+
+    g = torch.Generator().manual_seed(41)
+    S, c, o = 96, 256, 128
+    y = torch.randn(1, c, S, S, generator=g)
+    wo = torch.randn(c, c, generator=g) * c ** -0.5
+    bo = torch.randn(c, generator=g)
+    w0 = torch.randn(o, c, 3, 3, generator=g) * (9 * c) ** -0.5
+    b0 = torch.randn(o, generator=g)
+    yq = y.to(dt).float()
+    ref = F.conv2d(F.conv2d(yq, wo[:, :, None, None], bo), w0, b0, padding=1)[0].permute(1, 2, 0).reshape(S * S, o)
+    P = {k: v.to(cuda) for k, v in compose_head0(w0, b0, wo, bo, dt).items()}
+    x = yq[0].permute(1, 2, 0).reshape(S * S, c).contiguous().to(dt).to(cuda)
+    out = torch.full((S * S, o), float("nan"), dtype=dt, device=cuda)
+    ops.gemm(x, P["head.0c.w"], out, M=S * S, N=o, K=9 * c,
+             conv=dict(in_h=S, in_w=S, in_c=c, k=3, stride=1, pad=1, out_h=S, out_w=S),
+             bias=P["head.0c.b"], border_corr=P["head.0c.corr"], tile=DP_TILE_BIG_512x128)
+    close(out, ref, dt, "border-corrected composed conv")

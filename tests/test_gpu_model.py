@@ -83,10 +83,18 @@ def test_stage_parity(model, golden_dir):
     intermediates (tests/golden/golden_stages_frame0.npz, make_golden.py --stages)."""
     m, transform = model
     g = np.load(f"{golden_dir}/golden_stages_frame0.npz")
-    with torch.no_grad():
-        canonical, fov = m.forward(transform(frame(0)).unsqueeze(0))
     e = m.engine()
-    torch.cuda.synchronize()
+    # the decoder's out_conv output (fusion0 = the `feats` map) exists only on the uncomposed path
+    # (compose_head0 folds out_conv into head.0); the composed path's output is checked by
+    # test_forward_frame0_vs_reference
+    h0c, graph = e.head0_compose, e.graph
+    try:
+        e.head0_compose, e.graph = False, None
+        with torch.no_grad():
+            canonical, fov = m.forward(transform(frame(0)).unsqueeze(0))
+        torch.cuda.synchronize()
+    finally:
+        e.head0_compose, e.graph = h0c, graph
 
     def toks(buf, wins):
         t = buf.out.reshape(-1, 577, 1024)[wins][:, ::16, ::4]

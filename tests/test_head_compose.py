@@ -56,3 +56,37 @@ def test_compose_head_matches_reference_layer_order():
     assert got.shape == ref.shape
     err = (got - ref).abs().max().item()
     assert err < 1e-4 * (ref.abs().max().item() + 1), err
+
+
+def test_compose_head0_matches_out_conv_then_head0():
+    """engine.compose_head0: the decoder's 1x1 out_conv (decoder.py:184) followed by head.0's
+    3x3 zero-padded conv (depth_pro.py:182-207) == ONE 3x3 conv with the composed weights and
+    bias, minus the 1x1 bias's share of every tap that falls in the zero padding (what the
+    dp_gemm DP_STORE_ROWS border correction subtracts), evaluated in fp32 with torch ops."""
+    from depth_pro.engine import compose_head0
+
+    g = torch.Generator().manual_seed(3)
+    c, m, o, H, W = 64, 64, 128, 7, 9
+    y = torch.randn(1, c, H, W, generator=g)
+    wo = torch.randn(m, c, generator=g) * c ** -0.5
+    bo = torch.randn(m, generator=g)
+    w0 = torch.randn(o, m, 3, 3, generator=g) * (9 * m) ** -0.5
+    b0 = torch.randn(o, generator=g)
+    ref = F.conv2d(F.conv2d(y, wo[:, :, None, None], bo), w0, b0, padding=1)
+    P = compose_head0(w0, b0, wo, bo, torch.float32)
+    wc = P["head.0c.w"].float().reshape(o, c // 64, 3, 3, 64).permute(0, 1, 4, 2, 3).reshape(o, c, 3, 3)
+    got = F.conv2d(y, wc, padding=1) + P["head.0c.b"].reshape(1, o, 1, 1)
+    corr = P["head.0c.corr"].reshape(3, 3, o)
+    for a in range(3):
+        for b in range(3):
+            msk = torch.zeros(H, W, dtype=torch.bool)
+            if a == 0:
+                msk[0, :] = True
+            if a == 2:
+                msk[H - 1, :] = True
+            if b == 0:
+                msk[:, 0] = True
+            if b == 2:
+                msk[:, W - 1] = True
+            got = got - msk.float()[None, None] * corr[a, b].reshape(1, o, 1, 1)
+    assert torch.allclose(got, ref, atol=1e-4, rtol=1e-4), (got - ref).abs().max()
