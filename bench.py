@@ -32,10 +32,10 @@ PEAK_HBM_GBS = 8000.0
 
 
 TILE_NAMES = {1: "128x128", 2: "256x64", 3: "256x32", 4: "256x256", 5: "256x128", 8: "8phase-256x256",
-              12: "streamK-256x256", 13: "320x256", 14: "512x128"}
+              12: "streamK-256x256", 13: "320x256", 14: "512x128", 17: "dual-256x128"}
 TILE_KERNEL = {1: "gemm_kernel<{K}, 128, 128", 4: "gemm_big_kernel<{K}, 256, 256", 5: "gemm_big_kernel<{K}, 256, 128",
                8: "gemm_8ph_kernel<{K}", 12: "gemm_sk_kernel<{K}", 13: "gemm_big_kernel<{K}, 320, 256",
-               14: "gemm_big_kernel<{K}, 512, 128"}
+               14: "gemm_big_kernel<{K}, 512, 128", 17: "gemm_big_kernel<{K}, 256, 128, 32, 3"}
 
 
 def tile_kernel(tile: int, dtype: torch.dtype) -> str:
@@ -44,21 +44,23 @@ def tile_kernel(tile: int, dtype: torch.dtype) -> str:
     return t.format(K="KBF16" if dtype == torch.bfloat16 else "KF16") if t else ""
 
 
+# The PMC traffic summary the bench line cites (tools/pmc_traffic.py over separate FETCH_SIZE /
+# WRITE_SIZE passes of the tree being benched); named explicitly, updated with each profiled tree.
+PMC_TRAFFIC = "profiles/r03_pmc_traffic.json"
+
+
 def pmc_traffic(kernel: str, workgroups: int):
-    """HBM bytes per launch of `kernel` at `workgroups` from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json: tools/pmc_traffic.py over separate FETCH_SIZE / WRITE_SIZE passes,
-    FETCH_SIZE doubled per the gfx950 correction)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))
-    for path in reversed(files):
-        try:
-            data = json.load(open(path))
-        except (OSError, ValueError):
-            continue
-        for k in data.get("kernels", []):
-            if k["workgroups"] == workgroups and k["kernel"].startswith(kernel):
-                return {"bytes_per_launch": round(k["read_bytes_per_launch"] + k["write_bytes_per_launch"]),
-                        "source": os.path.relpath(path, REPO)}
+    """HBM bytes per launch of `kernel` at `workgroups` from PMC_TRAFFIC (FETCH_SIZE doubled per
+    the gfx950 correction), or None when that summary has no such launch."""
+    path = os.path.join(REPO, PMC_TRAFFIC)
+    try:
+        data = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    for k in data.get("kernels", []):
+        if k["workgroups"] == workgroups and k["kernel"].startswith(kernel):
+            return {"bytes_per_launch": round(k["read_bytes_per_launch"] + k["write_bytes_per_launch"]),
+                    "source": PMC_TRAFFIC}
     return None
 
 
@@ -106,11 +108,11 @@ def cpu_model() -> str:
 def cpu_baseline() -> dict:
     """The fp32 CPU oracle (a port of the reference path) on one synthetic frame.
 
-    Bounded sample (~20 s on 16 host threads): one untimed warm-up of a ViT block at
-    the patch-encoder shape's first window (thread pool + allocator), then one timed
-    frame through the oracle's `infer` (a full frame takes ~20 s, so a median of 3 would
-    push the default bench past its time budget; the box-to-box spread is reported
-    in DESIGN.md instead).
+    Bounded sample (~20 s on 16 host threads, BASELINE.md "CPU baseline"): one untimed
+    warm-up of a ViT block at the patch-encoder shape (thread pool + allocator), then one
+    timed frame through the oracle's `infer`.  One frame, not a median of three: a frame takes
+    ~20 s, and the baseline leg is bounded to 10-30 s of CPU work so that the default bench
+    finishes within minutes; the box-to-box spread is reported in DESIGN.md instead.
     """
     from depth_pro.weights import synthetic_state_dict
     from oracle import depth_pro_oracle as O
@@ -142,10 +144,6 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct resident frames per rank")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="1: frame pipeline (depth_pro.pipeline: frame i+1's image/FOV encoders beside frame i's "
-                         "decoder, two engines; measured slower, DESIGN.md 7); 0: one DepthPro.infer-style "
-                         "engine, frame by frame (default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,14 +171,9 @@ def main():
         packed = D.broadcast_packed(packed, dev, src=0)
     else:
         packed = pack_weights(synthetic_state_dict(0), dev, code)
-    if args.pipeline:
-        from depth_pro.pipeline import FramePipeline, u8_loader
-        pipe = FramePipeline(packed, dev, code, graph=not args.no_graph)
-        eng = pipe.E[0]
-    else:
-        eng = Engine(packed, dev, code)
-        if not args.no_graph:
-            eng.capture_graph()
+    eng = Engine(packed, dev, code)
+    if not args.no_graph:
+        eng.capture_graph()
     torch.cuda.synchronize()
     t_setup = time.time() - t_setup
 
@@ -193,8 +186,6 @@ def main():
     fpx = torch.empty((), dtype=torch.float32, device=dev)
     pending = [None, None]
 
-    if args.pipeline:
-        loaders = [u8_loader(f) for f in frames]
     counter = [0]
 
     def step(i):
@@ -204,12 +195,12 @@ def main():
             pending[i & 1] = None
         n = counter[0]
         counter[0] += 1
-        if args.pipeline:    # frame n's patch encoder + decoder, frame n+1's side encoders beside them
-            c, fov = pipe.step(loaders[n % len(frames)], loaders[(n + 1) % len(frames)])
-        else:
-            ops.normalize_u8(frames[n % len(frames)], eng.x0)
-            c, fov = eng.run()
-        ops.infer_epilogue(c, fov, None, 1536, 1536, d, fpx)
+        # DepthPro.infer's device work for a resident frame: normalise, forward, epilogue with the
+        # frame's health word, the asynchronous status snapshot (engine.FrameStatus)
+        ops.normalize_u8(frames[n % len(frames)], eng.x0)
+        c, fov = eng.run()
+        ops.infer_epilogue(c, fov, None, 1536, 1536, d, fpx, eng.status_dev[-1:])
+        eng.finish_status()
         if world > 1:
             _, pending[i & 1] = D.gather_frames(d, dst=0, async_op=True)
 
@@ -264,17 +255,13 @@ def main():
 
     parity = None
     if rank == 0:
-        if args.pipeline:    # a fresh two-frame stream starting at frame 0 (rank 0 holds frame 0)
-            pipe.primed = False
-            c, fov = pipe.step(loaders[0], loaders[1 % len(frames)])
-        else:
-            ops.normalize_u8(frames[0], eng.x0)
-            c, fov = eng.run()
-        ops.infer_epilogue(c, fov, None, 1536, 1536, depth, fpx)
+        ops.normalize_u8(frames[0], eng.x0)
+        c, fov = eng.run()
+        ops.infer_epilogue(c, fov, None, 1536, 1536, depth, fpx, eng.status_dev[-1:])
+        eng.finish_status()
         torch.cuda.synchronize()
         parity = depth_parity(depth, c, fov)
-        if args.pipeline:
-            pipe.check_status()
+        eng.check_status(block=True)     # every benched frame healthy (no timed-out hand-off, all finite)
 
     if rank == 0:
         achieved = fps_per_gpu * FLOP_PER_FRAME / 1e12
@@ -320,13 +307,8 @@ def main():
             "dtype": {"bf16": "bf16", "fp16": "f16", "mixed": "bf16+f16"}[args.dtype],
             "data": "synthetic (uint8 1536x1536 frames from numpy default_rng(k); synthetic seed-0 weights, "
                     "full Depth Pro architecture, 951,991,330 params)",
-            "config": {"workload": ("BASELINE config 3: steady-state 1536x1536 video stream, one frame per GPU "
-                                    "per step (patch+image+FOV ViT-L, decoder, heads, infer epilogue), frame "
-                                    "pipeline: frame i+1's image/FOV encoders beside frame i's decoder, hipGraph "
-                                    "replay of each phase") if args.pipeline else
-                                   ("BASELINE config 2/3: one 1536x1536 frame per GPU per step through "
+            "config": {"workload": ("BASELINE config 2/3: one 1536x1536 frame per GPU per step through "
                                     "DepthPro.infer (patch+image+FOV ViT-L, decoder, heads), hipGraph replay"),
-                       "pipeline": bool(args.pipeline),
                        "global_batch": world, "frame": [1536, 1536], "parallelism": f"frame-dp{world}",
                        "graph": not args.no_graph,
                        "precision": {"bf16": "bf16 everywhere", "fp16": "f16 everywhere",

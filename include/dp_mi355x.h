@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 6
+#define DP_ABI_VERSION 7
 int dp_abi_version(void);
 
 /*
@@ -128,7 +128,7 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
        DP_TILE_BIG_256x128_K32 = 7, DP_TILE_8PH_256x256 = 8, DP_TILE_DEEP4_256x256 = 9,
        DP_TILE_DEEP5_256x256 = 10, DP_TILE_DEEP_256x128 = 11, DP_TILE_STREAMK_256x256 = 12,
        DP_TILE_BIG_320x256 = 13, DP_TILE_BIG_512x128 = 14, DP_TILE_PBIG_320x256 = 15,
-       DP_TILE_PBIG_256x256 = 16 };
+       DP_TILE_PBIG_256x256 = 16, DP_TILE_DUAL_256x128 = 17 };
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 
@@ -143,13 +143,20 @@ int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
  * (bounded spin; the output of that launch is then wrong).  It is sticky: nothing
  * but the caller clears it, so one read after a whole forward / graph replay covers
  * every launch in it.  After a timeout the flags may be left set: zero the first 1 KiB
- * (or the whole workspace) before reusing it.  Bytes [2048, 3200) hold the tile-ticket
- * queues of the persistent data-parallel engine (8 per-XCD counters + an exit counter),
- * bytes [3200, 4088) the row-band counters of dp_gemm_ln's fused LayerNorm: both reset
- * to zero by the last workgroup that uses them in each launch.
+ * (or the whole workspace) before reusing it.
  */
 #define DP_GEMM_WS_ERROR_OFFSET 4092
 int64_t dp_gemm_workspace_size(void);
+
+/*
+ * dp_gemm_workspace_check: for the end of a forward (after every launch on `workspace`):
+ * *status (device int32) = the sticky error word; if it is set, the error word and every
+ * hand-off flag are zeroed, so the next forward starts clean and its own status reflects only
+ * its own launches.  One tiny kernel, graph-capturable.  (Reference: none -- the per-frame
+ * failure detection of SURVEY.md section 5 replacing the reference's per-frame try/except,
+ * generate_depth_maps.py:147-151.)
+ */
+int dp_gemm_workspace_check(void* workspace, int32_t* status, dp_stream_t stream);
 
 /*
  * Which engine / tile and how many workgroups dp_gemm would launch for `args`
@@ -157,26 +164,6 @@ int64_t dp_gemm_workspace_size(void);
  * persistent engine), *grid the workgroup count.  For tests and the bench.
  */
 int dp_gemm_plan(const dp_gemm_args* args, int32_t* tile, int32_t* grid);
-
-/*
- * dp_gemm_ln: dp_gemm, then y[r] = LN(C[r, 0:N]) * w + b (eps, two-pass-exact mean /
- * variance in fp32) written as `ln_dtype` rows of stride ld_ln -- the residual-stream
- * update of a timm Block followed by the NEXT LayerNorm (norm2 after attn.proj, the next
- * block's norm1 or the final norm after mlp.fc2: vision_transformer.py Block.forward,
- * reference network/vit_factory.py:68-124).  Requires DP_STORE_ROWS without a row-group
- * remap and an fp32 C.  When the launch fits one round of workgroups on the dense
- * 320x256 / 256x128 engines and `args->workspace` is set, the LayerNorm runs in the GEMM's
- * epilogue: each workgroup publishes per-row (mean, M2) partials of its columns, the
- * workgroups of a row band meet through counters in the workspace (bounded wait: a
- * timeout sets the sticky error word), and every workgroup normalises the rows it holds
- * in registers -- no fp32 re-read of C.  Otherwise the GEMM and a dp_layernorm pass run
- * back to back (same result up to fp32 summation order).  Because fused workgroups wait
- * for the rest of their band, never run two fused launches (or a fused launch and a
- * stream-K launch) concurrently on one device: each could hold the CUs the other's
- * undispatched workgroups need.  Beside kernels that do not wait it is safe.
- */
-int dp_gemm_ln(const dp_gemm_args* args, const float* ln_w, const float* ln_b, void* ln_out, int64_t ld_ln,
-               float eps, int32_t ln_dtype, dp_stream_t stream);
 
 /*
  * dp_layernorm: y[r] = LN(x[r]) * w + b over `cols`, fp32 in, 16-bit out.
@@ -265,12 +252,14 @@ int dp_fov_tail(const void* x6, int32_t dtype, const float* w, float bias, float
  *   f_px = use_given ? f_given : 0.5*W / tan(0.5*deg2rad(fov_deg))   (fp32)
  *   inv  = canonical * scale, scale = use_given ? (float)(W / f_given) : W / f_px
  *   inv  = bilinear(inv, (H, W)) when (H, W) != (1536, 1536)
- *   depth = 1 / clamp(inv, 1e-4, 1e4)                                  -> depth [H][W] fp32
- * f_px_out (device float) receives f_px.
+ *   depth = 1 / clamp(inv, 1e-4, 1e4)   (a NaN stays NaN, as torch.clamp)  -> depth [H][W] fp32
+ * f_px_out (device float) receives f_px.  nonfinite (optional device int32): incremented by the
+ * number of NaN / inf values written (depth and f_px) -- a per-frame health word the frame loops
+ * read back before writing a frame's files.
  */
 int dp_infer_epilogue(const float* canonical, int32_t src_h, int32_t src_w, const float* fov_deg,
                       int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
-                      float* f_px_out, dp_stream_t stream);
+                      float* f_px_out, int32_t* nonfinite, dp_stream_t stream);
 
 /*
  * dp_depth_to_points: camera-space point cloud of a depth map -- the reference's

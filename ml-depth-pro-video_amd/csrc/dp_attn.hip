@@ -19,7 +19,6 @@
 // through an exact per-tile-max pass), VALU row sums.
 // A last, partial key tile is masked and skips its empty 32-key half; one or two
 // leftover keys (the ViT's 577 = 9 x 64 + 1) go through the VALU instead (tail_key).
-#include <cstdlib>
 #include <type_traits>
 
 #include "dp_common.h"
@@ -57,34 +56,29 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
       : "memory");
 }
 
-// Running max (m_run, log2 units).  LAZY: set exactly by the first 32-key half tile
-// only; every later score is taken as P = 2^(s sl2 - m_run) with no max pass, no
-// compare and no rescale.  P only has to stay representable (16-bit B operand, fp32
-// sums), and a later key beyond that range (> ~127 log2 units above the first half
-// tile's max for bf16, > ~16 for f16) makes the row sum or O non-finite: the workgroup
-// then runs its keys again with EXACT, the per-half-tile max and deferred rescale
-// (m_run moves when exceeded by > 8, so P <= 256) -- rare on real inputs, checked once.
-// VSUM: row sums of P as f32 VALU adds (2 packed adds per 4 scores) instead of an MFMA
-// against an all-ones operand (4 MFMAs per 64-key tile).
-// PF: software-prefetched fragments -- a half tile's V^T fragments are read before its
-// softmax and the next half's K fragments before its PV MFMAs, so their LDS latency hides
-// under VALU / MFMA work of the same wave instead of one read-wait-MFMA round trip per
-// MFMA (+32 VGPRs: 3 workgroups per CU instead of 4).
-// PRE: the Q columns of qkv already hold Q * scale * log2(e) (dp_attention_log2q: the qkv
-// GEMM's per-column gamma), so scores come out of the MFMA in log2 units; once the lazy
-// running max is set, the S^T accumulator starts at -m_run instead of 0 and P = 2^S^T is ONE
-// v_exp_f32 per score (no v_fma_f32: a quarter of the softmax's VALU issue).
-// SADD (with VSUM): the row sums as ONE serial chain of v_add_f32 (nothing independent and
+// Running max (m_run, log2 units), set exactly by the first 32-key half tile only; every
+// later score is taken as P = 2^(s sl2 - m_run) with no max pass, no compare and no rescale.
+// P only has to stay representable (16-bit B operand, fp32 sums), and a later key beyond that
+// range (> ~127 log2 units above the first half tile's max for bf16, > ~16 for f16) makes the
+// row sum or O non-finite: the workgroup then runs its keys again on the exact path (the
+// per-half-tile max and deferred rescale: m_run moves when exceeded by > 8, so P <= 256) --
+// rare on real inputs, checked once.
+// Row sums of P: f32 VALU adds as ONE serial v_add_f32 chain (nothing independent and
 // isomorphic for the compiler to SLP-pack into v_pk_add_f32, which costs more issue beside
 // MFMAs).  Not inline asm: an asm add that reads a v_exp_f32 result right away misses the
 // transcendental-use wait state the compiler inserts for its own instructions.
-// NST: K/V ring depth.  3 = tile t+2's LDS-DMA issued at the top of tile t (two tiles of
-// compute cover each load; 48 KiB per workgroup: 3 workgroups per CU instead of 4).
-template <typename K_, bool LAZY, bool VSUM, bool PF, bool PRE = false, bool SADD = false, int NST = 2>
-__global__ void __launch_bounds__(256, (PF || NST == 3) ? 3 : 4)
+// PRE: the Q columns of qkv already hold Q * scale * log2(e) (dp_attention_log2q: the qkv
+// GEMM's per-column gamma), so scores come out of the MFMA in log2 units; once the running
+// max is set, the S^T accumulator starts at -m_run instead of 0 and P = 2^S^T is ONE v_exp_f32
+// per score.
+// Measured and rejected (round 2): software-prefetched fragments (3 workgroups per CU), a
+// 3-deep K/V ring, packed row-sum adds, row sums on the matrix core (profiles/r02l_attn_pf/,
+// r02z6_attn_nst3/, r02p_attn_sadd/).
+template <typename K_, bool PRE>
+__global__ void __launch_bounds__(256, 4)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
-  __shared__ __attribute__((aligned(1024))) char smem[NST][2 * TILE_B];   // [stage][K tile | V tile]
-  auto stage_of = [](int t) { return NST == 2 ? (t & 1) : (t % NST); };
+  __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
+  auto stage_of = [](int t) { return t & 1; };
   __shared__ int redo;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -147,25 +141,18 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     return v_off(row, byte);
   };
 
-  f32x16_t o[2], osum;         // osum (!VSUM): row sums of P from an all-ones A operand
-  f32x2_t lsum;                // VSUM: this lane's share of its query's row sum (its 32 of 64 keys)
-  float ls4[4];                // SADD: the same share as four partial sums
+  f32x16_t o[2];
+  float ls4[4];                // this lane's share of its query's row sum (its 32 of 64 keys)
   float m_run;
-  const uint32_t one2 = K_::pack2(1.f, 1.f);
-  const uint4 ones = make_uint4(one2, one2, one2, one2);
 
   auto rescale = [&](float m_upd) __attribute__((always_inline)) {   // m_run -> m_upd (>= m_run)
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_upd);
     #pragma unroll
     for (int i = 0; i < 16; ++i) {
       o[0][i] *= alpha; o[1][i] *= alpha;
-      if constexpr (!VSUM) osum[i] *= alpha;
     }
-    if constexpr (VSUM) lsum *= alpha;
-    if constexpr (SADD) {
-      #pragma unroll
-      for (int i = 0; i < 4; ++i) ls4[i] *= alpha;
-    }
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) ls4[i] *= alpha;
     m_run = m_upd;
   };
 
@@ -228,11 +215,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
           p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
         }
         w[jj] = K_::pack2(p0, p1);
-        if constexpr (SADD) {
-          ls4[0] = (ls4[0] + p0) + p1;
-        } else if constexpr (VSUM) {
-          lsum += f32x2_t{p0, p1};
-        }
+        ls4[0] = (ls4[0] + p0) + p1;
       }
       pf[st] = make_uint4(w[0], w[1], w[2], w[3]);
     }
@@ -248,98 +231,15 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
         const uint2 a = __builtin_bit_cast(uint2, lo), c = __builtin_bit_cast(uint2, up);
         o[db] = K_::mfma32(make_uint4(a.x, a.y, c.x, c.y), pf[st], o[db]);
       }
-      if constexpr (!VSUM) osum = K_::mfma32(ones, pf[st], osum);
     }
   };
-  // ---- PF variant of a half tile, in stages
-  auto read_k = [&](int t, int kb, uint4 (&kf)[4]) __attribute__((always_inline)) {
-    const char* K = smem[stage_of(t)];
-    #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
-  };
-  auto read_v = [&](int t, int kb, uint4 (&vf)[2][2]) __attribute__((always_inline)) {
-    const char* V = smem[stage_of(t)] + TILE_B;
-    #pragma unroll
-    for (int st = 0; st < 2; ++st)
-      #pragma unroll
-      for (int db = 0; db < 2; ++db) {
-        const int k0 = kb * 32 + 16 * st;
-        const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 0)));
-        const v4s_t up = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) v4s_t*)(V + vt_addr(db, k0, 1)));
-        const uint2 a = __builtin_bit_cast(uint2, lo), c = __builtin_bit_cast(uint2, up);
-        vf[st][db] = make_uint4(a.x, a.y, c.x, c.y);
-      }
-  };
-  // S^T, (mask), (max), softmax -> pf; then O^T += V^T P^T with the prefetched vf.  `knext`:
-  // the next half's K fragments are read between the softmax and the PV MFMAs.
-  auto half_pf = [&](int t, int kb, const uint4 (&kf)[4], auto partial_tag, bool setmax, bool exact,
-                     bool has_next, int tn, int kbn, uint4 (&knext)[4]) __attribute__((always_inline)) {
-    constexpr bool PARTIAL = decltype(partial_tag)::value;
-    const int kbase = t * KT;
-    f32x16_t s;
-    #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) s = K_::mfma32(kf[ks], qf[ks], ks == 0 ? f32x16_t{} : s);
-    uint4 vf[2][2];
-    read_v(t, kb, vf);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PARTIAL) {
-      #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-        if (key >= seq) s[r] = -INFINITY;
-      }
-    }
-    if (setmax) {
-      float mx = fmaxf(s[0], s[1]);
-      #pragma unroll
-      for (int r = 2; r < 16; ++r) mx = fmaxf(mx, s[r]);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      const float m_new = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sl2;
-      if (exact) {
-        if (__builtin_amdgcn_ballot_w64(m_new > m_run + 8.f)) rescale(fmaxf(m_run, m_new));
-      } else {
-        m_run = m_new;
-      }
-    }
-    uint4 pf[2];
-    #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      uint32_t w[4];
-      #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj], sl2, -m_run));
-        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
-        w[jj] = K_::pack2(p0, p1);
-        if constexpr (VSUM) lsum += f32x2_t{p0, p1};
-      }
-      pf[st] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    if (has_next) read_k(tn, kbn, knext);
-    __builtin_amdgcn_sched_barrier(0);
-    #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      #pragma unroll
-      for (int db = 0; db < 2; ++db) o[db] = K_::mfma32(vf[st][db], pf[st], o[db]);
-      if constexpr (!VSUM) osum = K_::mfma32(ones, pf[st], osum);
-    }
-  };
-
   // a 64-key tile = two halves; the second half of a partial tile is skipped when it holds no key
   auto do_tile = [&](int t, auto partial_tag, bool first, bool exact) __attribute__((always_inline)) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
     if (!active) return;
     const bool two = !PARTIAL || t * KT + 32 < seq;
-    if constexpr (PF) {
-      uint4 k0[4], k1[4];
-      read_k(t, 0, k0);
-      half_pf(t, 0, k0, partial_tag, exact || first, exact, two, t, 1, k1);
-      if (two) half_pf(t, 1, k1, partial_tag, exact, exact, false, t, 1, k0);
-    } else {
-      do_half(t, 0, partial_tag, exact || first, exact);
-      if (two) do_half(t, 1, partial_tag, exact, exact);
-    }
+    do_half(t, 0, partial_tag, exact || first, exact);
+    if (two) do_half(t, 1, partial_tag, exact, exact);
   };
 
   // One leftover key (seq = 64 n + r, r <= TAIL_VALU: the ViT's 577 = 9 x 64 + 1) costs a
@@ -370,9 +270,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     if (__builtin_amdgcn_ballot_w64(sc > m_run + 8.f)) rescale(fmaxf(m_run, sc));
     const float pr = __builtin_amdgcn_exp2f(sc - m_run);
     const float p = K_::to_f(K_::from_f(pr));
-    if constexpr (!VSUM) osum[0] += p;
-    else if constexpr (SADD) ls4[0] += 0.5f * p;
-    else lsum[0] += 0.5f * p;   // both half-waves add it: the swap below doubles it
+    ls4[0] += 0.5f * p;   // both half-waves add it: the swap in row_sum doubles it
     #pragma unroll
     for (int db = 0; db < 2; ++db)
       #pragma unroll
@@ -394,26 +292,16 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   const int nmma = valu_tail ? nfull : ntiles;     // tiles that go through the MFMAs
   auto run = [&](bool exact) __attribute__((always_inline)) {
     #pragma unroll
-    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; osum[i] = 0.f; }
-    lsum = f32x2_t{0.f, 0.f};
+    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
     #pragma unroll
     for (int i = 0; i < 4; ++i) ls4[i] = 0.f;
     m_run = -INFINITY;
     if (nmma > 0) issue(0, 0);
-    if constexpr (NST == 3) {
-      if (nmma > 1) issue(KT, 1);
-    }
-    // top of tile t: tile t landed (own pieces: counted vmcnt -- each issue is 4 pieces per
-    // thread; everyone's: the barrier, which also frees the stage of tile t-1 for the next issue)
+    // top of tile t: tile t landed (own pieces: vmcnt(0); everyone's: the barrier, which also
+    // frees the stage of tile t-1 for the next issue)
     auto top = [&](int t) __attribute__((always_inline)) {
-      if constexpr (NST == 3) {
-        if (t + 1 < nmma) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (t + 2 < nmma) issue((t + 2) * KT, stage_of(t + 2));
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        if (t + 1 < nmma) issue((t + 1) * KT, stage_of(t + 1));
-      }
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (t + 1 < nmma) issue((t + 1) * KT, stage_of(t + 1));
     };
     if (nfull > 0) {
       top(0);
@@ -432,16 +320,12 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     }
   };
   auto row_sum = [&]() __attribute__((always_inline)) {
-    if constexpr (VSUM) {
-      const float l = SADD ? (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]) : lsum[0] + lsum[1];
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
-      return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-    } else {
-      return osum[0];
-    }
+    const float l = (ls4[0] + ls4[1]) + (ls4[2] + ls4[3]);
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l), __float_as_uint(l), false, false);
+    return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   };
-  run(!LAZY);
-  if constexpr (LAZY) {
+  run(false);
+  {
     // a key far above the first half tile's max overflowed P, O or the row sum: all waves
     // of the workgroup take the exact path over their keys again (K/V restaged; rare)
     float chk = row_sum();
@@ -494,46 +378,14 @@ int attention_launch(const void* qkv, void* out, int32_t batch, int32_t seq, int
   // softmax(s * scale) = 2^(s * scale * log2 e) / sum: sl2 is the scale in log2 units
   const float sl2 = pre ? 1.0f : (float)((double)scale * 1.4426950408889634);
   hipStream_t s = (hipStream_t)stream;
-  // A/B switches: DP_ATTN_LAZY=0 takes the max of every half tile (the exact path);
-  // DP_ATTN_VSUM=0 takes the row sums on the matrix core; DP_ATTN_PF=1 prefetches the
-  // fragments (3 workgroups per CU).  Measured and rejected (round 2, profiles/r02l_attn_pf/):
-  // 35 x 577 76.9 / 79.5 us prefetched vs 75.4 / 75.3 us (frame 42.50 / 42.71 vs 42.73 / 42.70
-  // fps): the fourth workgroup per CU hides the read latency better than the in-wave prefetch.
-  static const bool lazy = [] { const char* e = getenv("DP_ATTN_LAZY"); return !(e && e[0] == '0'); }();
-  static const bool vsum = [] { const char* e = getenv("DP_ATTN_VSUM"); return !(e && e[0] == '0'); }();
-  static const bool pf = [] { const char* e = getenv("DP_ATTN_PF"); return e && e[0] == '1'; }();
   if (dtype != DP_BF16 && dtype != DP_F16) return DP_ERR_DTYPE;
-#define DP_ATTN(K, L, V) do { \
-    if (pf) hipLaunchKernelGGL((attn_kernel<K, L, V, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2); \
-    else hipLaunchKernelGGL((attn_kernel<K, L, V, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2); \
-  } while (0)
-#define DP_ATTN_K(K)                                                               \
-  do {                                                                             \
-    if (lazy) { if (vsum) DP_ATTN(K, true, true); else DP_ATTN(K, true, false); }  \
-    else { if (vsum) DP_ATTN(K, false, true); else DP_ATTN(K, false, false); }     \
-  } while (0)
-  // DP_ATTN_SADD=0: packed row-sum adds in the log2q kernel (A/B)
-  static const bool sadd = [] { const char* e = getenv("DP_ATTN_SADD"); return !(e && e[0] == '0'); }();
-  // DP_ATTN_NST=3: 3-deep K/V ring in the log2q kernel (A/B)
-  static const bool nst3 = [] { const char* e = getenv("DP_ATTN_NST"); return e && e[0] == '3'; }();
-  if (pre && sadd && nst3) {
-    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true, true, 3>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-    else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true, true, 3>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-  } else if (pre) {   // the default kernel (lazy max, VALU row sums) with log2-unit Q
-    if (sadd) {
-      if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-      else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-    } else {
-      if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-      else hipLaunchKernelGGL((attn_kernel<KF16, true, true, false, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-    }
-  } else if (dtype == DP_BF16) {
-    DP_ATTN_K(KBF16);
+  if (pre) {
+    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    else hipLaunchKernelGGL((attn_kernel<KF16, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
   } else {
-    DP_ATTN_K(KF16);
+    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    else hipLaunchKernelGGL((attn_kernel<KF16, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
   }
-#undef DP_ATTN_K
-#undef DP_ATTN
   DP_CHECK_LAUNCH();
   return 0;
 }

@@ -60,17 +60,6 @@ struct GemmP {
   int tiles_n, tiles_m;
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
   unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
-  unsigned* tq;      // persistent engine: tile-ticket queues in the workspace (NULL: static tile walk)
-  // fused LayerNorm of the rows of C (dp_gemm_ln): gemm_big_kernel<..., LNF = true> only
-  const float* ln_w;
-  const float* ln_b;
-  u16* ln_out;
-  long long ld_ln;
-  float ln_eps;
-  int ln_f16;        // LN output kind: 1 f16, 0 bf16
-  unsigned long long* ln_part;  // [N / TN][M] (mean, M2) pairs of every wave's TN columns
-  unsigned* ln_cnt;  // per row band: arrivals, departures
-  unsigned* err;     // sticky workspace error word
 };
 
 // Process-wide ablation / fault-injection bits, set only by dp_gemm_debug_flags (tools and
@@ -662,23 +651,26 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
   }
 }
 
-template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, bool LNF = false>
-__global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
+// NW = waves per workgroup: 8 (one workgroup per CU), or 4 (two workgroups per CU, each
+// wave one per SIMD: one workgroup's epilogue runs beside the other's K loop).
+template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, int NW = 8>
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(const GemmP p) {
   // 8 waves as WM x WN; the 512 x 128 tile (N = 128 layers) uses 4 x 2 so that every
-  // wave still owns a 128 x 64 sub-tile (same fragment reuse as the 256 x 256 tile)
-  constexpr int WN = BM == 512 ? 2 : 4, WM = 8 / WN;
+  // wave still owns a 128 x 64 sub-tile (same fragment reuse as the 256 x 256 tile);
+  // 4 waves as 2 x 2 (256 x 128: 128 x 64 per wave)
+  constexpr int WN = NW == 4 ? 2 : (BM == 512 ? 2 : 4), WM = NW / WN;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
   constexpr int RB = BKT * 2;                 // LDS row bytes
   constexpr int CR = BKT / 8;                 // 16-B chunks per row
   constexpr int ROWS_PER_WAVE_PIECE = 1024 / RB;
-  constexpr int ROWS_PER_ROUND = 8 * ROWS_PER_WAVE_PIECE;  // rows covered by one piece of every wave
+  constexpr int ROWS_PER_ROUND = NW * ROWS_PER_WAVE_PIECE;  // rows covered by one piece of every wave
   constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int LA = BM / ROWS_PER_ROUND;     // LDS-DMA pieces per thread per A tile
   constexpr int LB = BN / ROWS_PER_ROUND;
   constexpr int LT = LA + LB;
-  constexpr int EPI_BYTES = 8 * 32 * (TN + 4) * 4;  // epilogue staging (8 waves x 32 fp32 rows)
+  constexpr int EPI_BYTES = NW * 32 * (TN + 4) * 4;  // epilogue staging (NW waves x 32 fp32 rows)
   constexpr int SMEM = NS * STAGE > EPI_BYTES ? NS * STAGE : EPI_BYTES;
   static_assert(NS >= 2 && SMEM <= 160 * 1024 && LB >= 1, "LDS ring");
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -737,10 +729,10 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
       } else {
         src = a_src[i] + k0;
       }
-      glds16(src, sa + i * 8192);
+      glds16(src, sa + i * NW * 1024);
     }
     #pragma unroll
-    for (int i = 0; i < LB; ++i) glds16(b_src[i] + k0, sb + i * 8192);
+    for (int i = 0; i < LB; ++i) glds16(b_src[i] + k0, sb + i * NW * 1024);
   };
 
   f32x4_t acc[FM][FN];
@@ -945,129 +937,13 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
         for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
         ms[it] = m0 + wm * TM + q * 32 + row;
       }
-      if constexpr (TN % 32 == 0 && !LNF) {
+      if constexpr (TN % 32 == 0) {
         if (p.store_mode == DP_STORE_HEAD_PS) {
           head_ps_rows<NITC>(p, cc, ms, n_l, v, lane);
           continue;
         }
       }
       epilogue_rows<K_, NITC, CONV && BM == 512 && !RELU>(p, cc, ms, n_l, v);
-      if constexpr (LNF) {
-        // the new rows stay in the registers of the accumulators this pass consumed
-        // (8 * FN floats per lane per pass, same count), and each wave publishes, per row,
-        // the mean and centred sum of squares of its TN columns (Chan's pairwise form)
-        #pragma unroll
-        for (int it = 0; it < NITC; ++it) {
-          float sm = 0.f;
-          #pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const int idx = (c0 + it) * 8 + r;
-            acc[2 * q + idx / (4 * FN)][(idx % (4 * FN)) / 4][idx % 4] = v[it][r];
-            sm += v[it][r];
-          }
-          #pragma unroll
-          for (int o = 1; o < CPR; o <<= 1) sm += __shfl_xor(sm, o);
-          const float mw = sm * (1.f / TN);
-          float m2 = 0.f;
-          #pragma unroll
-          for (int r = 0; r < 8; ++r) m2 += (v[it][r] - mw) * (v[it][r] - mw);
-          #pragma unroll
-          for (int o = 1; o < CPR; o <<= 1) m2 += __shfl_xor(m2, o);
-          if (lane % CPR == 0 && ms[it] < p.M) {
-            const unsigned long long pk = (unsigned long long)__float_as_uint(mw) |
-                                          ((unsigned long long)__float_as_uint(m2) << 32);
-            __hip_atomic_store(p.ln_part + (long long)(tile_n * WN + wn) * p.M + ms[it], pk, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);   // write-through: read by other XCDs
-          }
-        }
-      }
-    }
-  }
-  if constexpr (LNF) {
-    // Band hand-off (the tiles_n workgroups of this row band, all resident: the host only
-    // fuses single-round grids): publish -- every wave's partial stores done, then ONE
-    // agent-scope arrival add -- and wait for the band's other arrivals (bounded spin:
-    // a timeout sets the sticky error word and the LN rows of this band are wrong).
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned* const arr = p.ln_cnt + 2 * tile_m;
-    if (tid == 0) {
-      __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      unsigned n = 0;
-      while (__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)p.tiles_n) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++n == (1u << 22)) {
-          __hip_atomic_fetch_or(p.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    // per row: mean and M2 of all N / TN partials (each lane of the row's CPR lanes combines
-    // every CPR-th partial), then (x - mean) * rstd * w + b -> 16-bit, 16-B stores
-    const int P = p.N / TN, c_ = lane % CPR;
-    float lw[8], lb[8];
-    {
-      const int nc = n_l < p.N ? n_l : p.N - 8;
-      const float4 w0 = *(const float4*)(p.ln_w + nc), w1 = *(const float4*)(p.ln_w + nc + 4);
-      const float4 b0 = *(const float4*)(p.ln_b + nc), b1 = *(const float4*)(p.ln_b + nc + 4);
-      lw[0] = w0.x; lw[1] = w0.y; lw[2] = w0.z; lw[3] = w0.w; lw[4] = w1.x; lw[5] = w1.y; lw[6] = w1.z; lw[7] = w1.w;
-      lb[0] = b0.x; lb[1] = b0.y; lb[2] = b0.z; lb[3] = b0.w; lb[4] = b1.x; lb[5] = b1.y; lb[6] = b1.z; lb[7] = b1.w;
-    }
-    const float inv_n = 1.f / (float)p.N;
-    #pragma unroll
-    for (int q = 0; q < FM / 2; ++q) {
-      #pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int m = m0 + wm * TM + q * 32 + it * RPI + lane / CPR;
-        const int mc = m < p.M ? m : p.M - 1;
-        float smean = 0.f, ssq = 0.f, ms_[8], m2_[8];
-        int np = 0;
-        #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int j = c_ + k * CPR;
-          if (j < P) {
-            const unsigned long long pk =
-                __hip_atomic_load(p.ln_part + (long long)j * p.M + mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ms_[k] = __uint_as_float((unsigned)pk);
-            m2_[k] = __uint_as_float((unsigned)(pk >> 32));
-            smean += ms_[k];
-            ++np;
-          }
-        }
-        #pragma unroll
-        for (int o = 1; o < CPR; o <<= 1) smean += __shfl_xor(smean, o);
-        const float mean = smean / (float)P;
-        #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k < np) ssq += m2_[k] + (float)TN * (ms_[k] - mean) * (ms_[k] - mean);
-        #pragma unroll
-        for (int o = 1; o < CPR; o <<= 1) ssq += __shfl_xor(ssq, o);
-        const float rstd = rsqrtf(ssq * inv_n + p.ln_eps);
-        float h[8];
-        #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int idx = it * 8 + r;
-          h[r] = (acc[2 * q + idx / (4 * FN)][(idx % (4 * FN)) / 4][idx % 4] - mean) * rstd * lw[r] + lb[r];
-        }
-        uint4 o;
-        if (p.ln_f16) {
-          o.x = KF16::pack2(h[0], h[1]); o.y = KF16::pack2(h[2], h[3]);
-          o.z = KF16::pack2(h[4], h[5]); o.w = KF16::pack2(h[6], h[7]);
-        } else {
-          o.x = KBF16::pack2(h[0], h[1]); o.y = KBF16::pack2(h[2], h[3]);
-          o.z = KBF16::pack2(h[4], h[5]); o.w = KBF16::pack2(h[6], h[7]);
-        }
-        if (m < p.M && n_l < p.N) *(uint4*)(p.ln_out + (long long)m * p.ld_ln + n_l) = o;
-      }
-    }
-    // departures: the band's last workgroup out resets both counters for the next launch
-    if (tid == 0) {
-      const unsigned d = __hip_atomic_fetch_add(arr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == (unsigned)p.tiles_n - 1u) {
-        __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(arr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
   }
   DP_STAMP(st3_);
@@ -1088,34 +964,6 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_big_kernel(const GemmP p) {
 // ROWLD: the epilogue reads per-row operands (residuals, pos, the fp32 C being accumulated
 // into); without them it needs fewer VGPRs (the 320 x 256 tile is at the 256 limit).
 //
-// Dynamic tile queues (p.tq != NULL, K >= 3 steps): instead of the static walk wgid,
-// wgid + G, ... every workgroup draws its tiles from the queue of the XCD it runs on
-// (8 agent-scope ticket counters).  Queue x hands out, round by round, the tile
-// positions [x*G/8, (x+1)*G/8) of each round of G tiles -- the same XCD-contiguous
-// placement as the static walk -- and a workgroup whose own queue is empty takes from
-// the next XCD's.  A workgroup that starts late (its CU still held by a side-stream
-// kernel) therefore just takes fewer tiles instead of ending the launch on a tail.
-// The ticket for the next tile is drawn at K step 0 of the current one and read back at
-// step 1 (its latency hides under the K loop), published through an LDS word.  The
-// last workgroup to finish resets the counters (graph-replay safe, no memset).
-constexpr int TQ_BYTE_OFF = 2048;   // workspace byte offset: 8 queues + exit counter, 128 B apart
-constexpr int TQ_STRIDE = 32;       // uint32 words between counters
-__device__ __forceinline__ int tq_map(int G, int T, int x, unsigned k) {
-  const int c0 = x * G / 8, len = (x + 1) * G / 8 - c0;
-  if (len <= 0) return -1;
-  const long long t = (long long)(k / (unsigned)len) * G + c0 + (int)(k % (unsigned)len);
-  return t < T ? (int)t : -1;
-}
-// thread-0 only: tickets from queue home+q, home+q+1, ... until a valid tile or all 8 are empty
-__device__ __forceinline__ int tq_draw(unsigned* tq, int G, int T, int home, int& q) {
-  for (; q < 8; ++q) {
-    const int x = (home + q) & 7;
-    const unsigned k = __hip_atomic_fetch_add(tq + TQ_STRIDE * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int t = tq_map(G, T, x, k);
-    if (t >= 0) return t;
-  }
-  return -1;
-}
 template <typename K_, int BM, int BN, bool CONV, bool RELU, bool ROWLD>
 __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
   constexpr int BKT = 64, WN = 4, WM = 2;
@@ -1129,10 +977,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
   constexpr int CPR = TN / 8, RPI = 64 / CPR, NIT = PR / RPI;
   constexpr int STORES = (FM * 16 / PR) * NIT;                   // 16-B stores per lane per tile (16-bit C)
   static_assert(8 * PR * SROW * 4 <= STAGE && FM % (PR / 16) == 0 && NIT % 2 == 0, "staging");
-  // ONE LDS array (ring + the tile-ticket word): a second __shared__ object can make hipcc
-  // put a vmcnt(0) in front of the loop's ds_reads
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 16];
-  int* const tslot = (int*)(smem + 2 * STAGE);
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6;
@@ -1140,42 +985,14 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
   const int wm = wave / WN, wn = wave % WN;
   const int G = gridDim.x, bid = blockIdx.x;
   const int T = p.tiles_m * p.tiles_n;
-  const bool dyn = p.tq != nullptr;
-  int t_begin;
-  int home = 0, tq_q = 0;      // thread 0: home queue, queues found empty so far
-  unsigned tq_k = 0;           // thread 0: ticket drawn at K step 0
-  if (dyn) {
-    if (tid == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      home = (int)(xcc & 7);
-      tslot[0] = tq_draw(p.tq, G, T, home, tq_q);
-    }
-    lds_barrier();
-    t_begin = __builtin_amdgcn_readfirstlane(tslot[0]);
-  } else {
-    // static walk: this workgroup's tiles are wgid, wgid + G, ...: at any moment the
-    // workgroups of one XCD (consecutive wgids) work on consecutive tiles of the band
-    // raster, as the rounds of the data-parallel launch do (shared A / B panels in that
-    // XCD's L2)
-    const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    t_begin = wgid < T ? wgid : -1;
-  }
-  // every workgroup counts itself out; the last one resets the queues for the next launch
-  auto leave = [&]() {
-    if (dyn && tid == 0) {
-      const unsigned d = __hip_atomic_fetch_add(p.tq + TQ_STRIDE * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == (unsigned)G - 1u) {
-        #pragma unroll
-        for (int x = 0; x <= 8; ++x) __hip_atomic_store(p.tq + TQ_STRIDE * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  };
-  if (t_begin < 0) {
-    leave();
-    return;
-  }
+  // static walk: this workgroup's tiles are wgid, wgid + G, ...: at any moment the
+  // workgroups of one XCD (consecutive wgids) work on consecutive tiles of the band
+  // raster, as the rounds of the data-parallel launch do (shared A / B panels in that
+  // XCD's L2)
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  if (wgid >= T) return;
+  const int t_begin = wgid;
 
   const int prow = wave * 8 + (lane >> 3);
   const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
@@ -1275,28 +1092,9 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
       if (kt == 0 && !first) wait_vmcnt<STORES>();
       else wait_vmcnt<0>();
       lds_barrier();
-      if (dyn && tid == 0) {
-        // next tile's ticket: drawn at step 0, resolved at step 1 (after its vmcnt(0)),
-        // read by every wave at step KT-1 >= 2, behind a barrier
-        if (kt == 0 && tq_q < 8)
-          tq_k = __hip_atomic_fetch_add(p.tq + TQ_STRIDE * ((home + tq_q) & 7), 1u, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        if (kt == 1) {
-          int tn_ = -1;
-          if (tq_q < 8) {
-            tn_ = tq_map(G, T, (home + tq_q) & 7, tq_k);
-            if (tn_ < 0) {
-              ++tq_q;
-              tn_ = tq_draw(p.tq, G, T, home, tq_q);
-            }
-          }
-          tslot[0] = tn_;
-        }
-      }
       if (kt + 1 < KT) {
         issue(kt + 1, stage ^ 1);
       } else {
-        if (dyn) t_next = __builtin_amdgcn_readfirstlane(tslot[0]);
         if (t_next >= 0) {
           tile_coords(p, t_next, tm, tn);
           m0n = tm * BM;
@@ -1350,7 +1148,6 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
     m0 = m0n;
     n0 = n0n;
   }
-  leave();
 }
 
 // ======================================================= 8-phase 256x256 engine
@@ -1508,6 +1305,13 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
   }
   if (wm == 0) bar();
   if (sprio) __builtin_amdgcn_s_setprio(0);
+  if (p.dbg & 1) {   // ablation (tools/gemm_bench.py --ablate): no epilogue
+    #pragma unroll
+    for (int i = 0; i < 8; ++i)
+      #pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j][0]), "v"(acc[i][j][1]), "v"(acc[i][j][2]), "v"(acc[i][j][3]));
+    return;
+  }
 
   // epilogue: identical to the big engine (LDS-staged, row-coalesced)
   lds_barrier();
@@ -2007,18 +1811,6 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_m = (p.M + BM - 1) / BM;
   dim3 grid(p.tiles_n * p.tiles_m);
-  // fused LayerNorm epilogue (dp_gemm_ln): only the dense residual-accumulate engines of the
-  // ViT proj / fc2 GEMMs have an LNF instantiation; dp_gemm_ln checks eligibility first
-  if (p.ln_out) {
-    if constexpr (BKT == 64 && ((BM == 320 && BN == 256 && !PIPE) || (BM == 256 && BN == 128 && PIPE))) {
-      if (conv || p.relu_a) return DP_ERR_ARG;
-      hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, false, true>), grid, dim3(NT_BIG), 0, s,
-                         p);
-      DP_CHECK_LAUNCH();
-      return 0;
-    }
-    return DP_ERR_ARG;
-  }
   if (conv && p.relu_a)
     hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, true, true>), grid, dim3(NT_BIG), 0, s, p);
   else if (conv)
@@ -2027,6 +1819,25 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
     hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, true>), grid, dim3(NT_BIG), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, false>), grid, dim3(NT_BIG), 0, s, p);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+// two 4-wave workgroups per CU (tile 256 x 128, BK 32, 3-stage ring)
+template <typename K_>
+int launch_dual(const GemmP& p0, bool conv, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = (p.N + 127) / 128;
+  p.tiles_m = (p.M + 255) / 256;
+  dim3 grid(p.tiles_n * p.tiles_m);
+  if (conv && p.relu_a)
+    hipLaunchKernelGGL((gemm_big_kernel<K_, 256, 128, 32, 3, false, true, true, 4>), grid, dim3(256), 0, s, p);
+  else if (conv)
+    hipLaunchKernelGGL((gemm_big_kernel<K_, 256, 128, 32, 3, false, true, false, 4>), grid, dim3(256), 0, s, p);
+  else if (p.relu_a)
+    hipLaunchKernelGGL((gemm_big_kernel<K_, 256, 128, 32, 3, false, false, true, 4>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_big_kernel<K_, 256, 128, 32, 3, false, false, false, 4>), grid, dim3(256), 0, s, p);
   DP_CHECK_LAUNCH();
   return 0;
 }
@@ -2075,6 +1886,7 @@ int launch_k(const GemmP& p, int tile, bool conv, hipStream_t s) {
     case DP_TILE_DEEP_256x128: return launch_big<K_, 256, 128, 32, 6, false>(p, conv, s);
     case DP_TILE_BIG_320x256: return launch_big<K_, 320, 256, 64, 2, false>(p, conv, s);
     case DP_TILE_BIG_512x128: return launch_big<K_, 512, 128, 64, 2, false>(p, conv, s);
+    case DP_TILE_DUAL_256x128: return launch_dual<K_>(p, conv, s);
     default: return launch_big<K_, 256, 256, 64, 2, false>(p, conv, s);
   }
 }
@@ -2094,6 +1906,26 @@ extern "C" int dp_gemm_debug_flags(int flags) {
 }
 
 extern "C" int64_t dp_gemm_workspace_size(void) { return SK_FLAG_BYTES + (int64_t)SK_MAX_WG * SK_TILE_F * 4; }
+
+namespace {
+// After a forward (every launch that used `ws` has ended): report the sticky error word and,
+// if it is set, clear it and every hand-off flag (a producer that published after its consumer
+// gave up leaves its flag set; the next launch would read it as a fresh hand-off).
+__global__ void ws_check_kernel(uint32_t* __restrict__ ws, int32_t* __restrict__ status) {
+  const uint32_t err = ws[DP_GEMM_WS_ERROR_OFFSET / 4];
+  if (threadIdx.x == 0) status[0] = (int32_t)err;
+  if (err == 0) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < (int)(SK_FLAG_BYTES / 4); i += blockDim.x) ws[i] = 0u;
+}
+}  // namespace
+
+extern "C" int dp_gemm_workspace_check(void* workspace, int32_t* status, dp_stream_t stream) {
+  if (!workspace || !status) return DP_ERR_ARG;
+  hipLaunchKernelGGL(ws_check_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (uint32_t*)workspace, status);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
 
 namespace {
 // Validate the arguments, fill the kernel parameters and pick the engine.
@@ -2120,7 +1952,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   if (a->store_mode == DP_STORE_ROWS && a->head_corr) {
     // composed conv with border correction: a stride-1, pad-1 3x3 implicit conv, rows = pixels
+    // (no ReLU prologue: the correction is compiled into the non-ReLU conv instantiation only)
     if (a->a_mode != DP_A_CONV || a->k_h != 3 || a->k_w != 3 || a->pad != 1 || a->stride != 1 || a->head_w ||
+        a->relu_a ||
         a->row_group || a->out_h != a->in_h || a->out_w != a->in_w || a->N % 8 != 0 || a->N < 128 ||
         (a->tile != DP_TILE_AUTO && a->tile <= DP_TILE_256x32))   // the small engines have no correction
       return DP_ERR_ARG;
@@ -2211,14 +2045,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     // dense (ViT) GEMMs only with debug 2048: they run beside the side encoders, and a
     // persistent grid whose workgroups cannot all start at once ends on a tail (qkv: 146 ->
     // 140 us alone, frame 23.74 -> 23.89 ms in-frame)
-    // debug 4096: persistent grids draw their tiles from per-XCD queues (a late workgroup
-    // takes fewer tiles), dense GEMMs included.  Measured and rejected (round 2, same box,
-    // graph replay, 2 x 4 runs): 42.55 / 42.65 fps off; queues + persistent qkv 42.27 /
-    // 42.13; + fc1 on the persistent 320 x 256 42.0 / 42.0, on 256 x 256 41.9 / 41.95.  Eager
-    // serial: qkv 136.5 (data-parallel 320 x 256) vs 139.4 us, fc1 195.8 (8-phase) vs 196.4
-    // / 199.8 us, 768^2 conv 711 vs 712 us (profiles/r02i_tile_queues/).
-    const bool dyn_ok = ws_ok && a->K / 64 >= 3 && (dbg & 4096);
-    const bool dense_ok = a->a_mode == DP_A_CONV || (dbg & 2048) || dyn_ok;
+    const bool dense_ok = a->a_mode == DP_A_CONV || (dbg & 2048);
     if (dense_ok && tile == DP_TILE_BIG_320x256 && (long long)((a->M + 319) / 320) * (a->N / 256) >= 2 * ncu)
       tile = DP_TILE_PBIG_320x256;
     else if (dense_ok && tile == DP_TILE_BIG_256x256 && tiles256 >= 2 * ncu)
@@ -2249,14 +2076,6 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   p.dbg = dbg;
   p.c_bytes = c_bytes;
-  p.tq = nullptr;
-  p.ln_w = p.ln_b = nullptr; p.ln_out = nullptr; p.ld_ln = 0; p.ln_eps = 0.f; p.ln_f16 = 0;
-  p.ln_part = nullptr; p.ln_cnt = nullptr; p.err = nullptr;
-  // persistent launches with a workspace and >= 3 K steps take their tiles from the queues:
-  // debug 4096 (measured slower, above), or an explicit PBIG tile hint with a workspace
-  if ((tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) && ws_ok && a->K / 64 >= 3 &&
-      ((dbg & 4096) || a->tile != DP_TILE_AUTO))
-    p.tq = (unsigned*)((char*)a->workspace + TQ_BYTE_OFF);
   return 0;
 }
 }  // namespace
@@ -2275,6 +2094,7 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
     case DP_TILE_BIG_256x128: case DP_TILE_BIG_256x128_K32: case DP_TILE_DEEP_256x128: bn = 128; break;
     case DP_TILE_BIG_320x256: bm = 320; bn = 256; break;
     case DP_TILE_BIG_512x128: bm = 512; bn = 128; break;
+    case DP_TILE_DUAL_256x128: bn = 128; break;
     case DP_TILE_PBIG_320x256: bm = 320; bn = 256; break;
     default: bn = 256;
   }
@@ -2283,47 +2103,6 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
   if (tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) grid = grid < num_cus() ? grid : num_cus();
   if (grid_out) *grid_out = tile == DP_TILE_STREAMK_256x256 ? sk_grid(p) : grid;
   return 0;
-}
-
-// byte offset of the fused-LN band counters in the workspace (after the tile queues, before
-// the error word): 2 words per row band
-constexpr int LN_CNT_OFF = 3200, LN_MAX_BANDS = (DP_GEMM_WS_ERROR_OFFSET - LN_CNT_OFF) / 8;
-
-extern "C" int dp_gemm_ln(const dp_gemm_args* a, const float* ln_w, const float* ln_b, void* ln_out, int64_t ld_ln,
-                          float eps, int32_t ln_dtype, dp_stream_t stream) {
-  if (!a || !ln_w || !ln_b || !ln_out) return DP_ERR_ARG;
-  if (ln_dtype != DP_BF16 && ln_dtype != DP_F16) return DP_ERR_DTYPE;
-  if (a->store_mode != DP_STORE_ROWS || a->row_group || a->c_dtype != DP_F32 || a->head_w || ld_ln < a->N ||
-      ld_ln % 8 != 0 || ((uintptr_t)ln_out & 15))
-    return DP_ERR_ARG;
-  GemmP p;
-  int tile = 0;
-  int rc = gemm_plan(a, p, tile);
-  if (rc) return rc;
-  const int bm = tile == DP_TILE_BIG_320x256 ? 320 : 256, bn = tile == DP_TILE_BIG_320x256 ? 256 : 128;
-  const long long tm = (a->M + bm - 1) / bm, tn = a->N / bn;
-  const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
-  // fused: one of the two LNF engines, a single round of workgroups (every workgroup of a row
-  // band resident at once, so the band hand-off cannot wait on an undispatched one), N a
-  // whole number of tiles (every column's partial written)
-  const bool fuse = (tile == DP_TILE_BIG_320x256 || tile == DP_TILE_BIG_256x128) && a->a_mode == DP_A_DENSE &&
-                    !a->relu_a && ws_ok && a->N % bn == 0 && tm * tn <= num_cus() && tm <= LN_MAX_BANDS &&
-                    (long long)a->N / (bn / 4) * a->M * 8 <= a->workspace_bytes - SK_FLAG_BYTES &&
-                    !(p.dbg & 65536);
-  hipStream_t s = (hipStream_t)stream;
-  if (!fuse) {   // unfused: the GEMM, then the LayerNorm pass over C
-    rc = dp_gemm(a, stream);
-    if (rc) return rc;
-    return dp_layernorm((const float*)a->C, a->ldc, ln_w, ln_b, ln_out, ld_ln, a->M, a->N, eps, ln_dtype, stream);
-  }
-  char* ws = (char*)a->workspace;
-  p.ln_w = ln_w; p.ln_b = ln_b; p.ln_out = (u16*)ln_out; p.ld_ln = ld_ln; p.ln_eps = eps;
-  p.ln_f16 = ln_dtype == DP_F16;
-  p.ln_part = (unsigned long long*)(ws + SK_FLAG_BYTES);
-  p.ln_cnt = (unsigned*)(ws + LN_CNT_OFF);
-  p.err = (unsigned*)(ws + DP_GEMM_WS_ERROR_OFFSET);
-  if (a->dtype == DP_BF16) return launch_k<KBF16>(p, tile, false, s);
-  return launch_k<KF16>(p, tile, false, s);
 }
 
 extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {

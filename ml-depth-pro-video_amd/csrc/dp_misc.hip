@@ -290,7 +290,7 @@ __global__ void fov_tail_kernel(const u16* __restrict__ x6, const float* __restr
 // ------------------------------------------------------------ infer epilogue
 __global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW, const float* __restrict__ fov,
                                  int use_given, float given_scale, float given_fpx, int H, int W,
-                                 float* __restrict__ depth, float* __restrict__ fpx_out) {
+                                 float* __restrict__ depth, float* __restrict__ fpx_out, int* __restrict__ nonfinite) {
   float fpx, scale;
   if (use_given) {
     fpx = given_fpx;
@@ -302,7 +302,10 @@ __global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW
     scale = (float)W / fpx;
   }
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0 && fpx_out) fpx_out[0] = fpx;
+  if (i == 0) {
+    if (fpx_out) fpx_out[0] = fpx;
+    if (nonfinite && !__builtin_isfinite(fpx)) atomicAdd(nonfinite, 1);
+  }
   if (i >= (long long)H * W) return;
   float v;
   if (H == SH && W == SW) {
@@ -317,8 +320,15 @@ __global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW
     const float v10 = canon[(long long)y1 * SW + x0] * scale, v11 = canon[(long long)y1 * SW + x1] * scale;
     v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
   }
-  v = fminf(fmaxf(v, 1e-4f), 1e4f);
-  depth[i] = 1.0f / v;
+  // torch.clamp keeps a NaN a NaN (fminf / fmaxf alone would turn it into a bound)
+  v = v != v ? v : fminf(fmaxf(v, 1e-4f), 1e4f);
+  const float d = 1.0f / v;
+  depth[i] = d;
+  if (nonfinite) {
+    // one add per wave that saw a NaN / inf (a healthy frame issues none)
+    const unsigned long long bad = __ballot(!__builtin_isfinite(d));
+    if (bad && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(bad)) atomicAdd(nonfinite, (int)__builtin_popcountll(bad));
+  }
 }
 
 inline int blocks_for(long long n, int bs) { return (int)((n + bs - 1) / bs); }
@@ -430,13 +440,14 @@ extern "C" int dp_fov_tail(const void* x6, int32_t dtype, const float* w, float 
 
 extern "C" int dp_infer_epilogue(const float* canonical, int32_t SH, int32_t SW, const float* fov_deg,
                                  int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
-                                 float* f_px_out, dp_stream_t stream) {
+                                 float* f_px_out, int32_t* nonfinite, dp_stream_t stream) {
   if (!canonical || !depth || (!use_given && !fov_deg)) return DP_ERR_ARG;
   if (H <= 0 || W <= 0 || SH <= 0 || SW <= 0) return DP_ERR_SHAPE;
   // reference: inverse_depth = canonical * (W / f_px) with W / f_px a Python (double) scalar
   const float given_scale = use_given ? (float)((double)W / f_given) : 0.f;
   hipLaunchKernelGGL(infer_epi_kernel, dim3(blocks_for((long long)H * W, 256)), dim3(256), 0, (hipStream_t)stream,
-                     canonical, SH, SW, fov_deg, use_given, given_scale, (float)f_given, H, W, depth, f_px_out);
+                     canonical, SH, SW, fov_deg, use_given, given_scale, (float)f_given, H, W, depth, f_px_out,
+                     (int*)nonfinite);
   DP_CHECK_LAUNCH();
   return 0;
 }

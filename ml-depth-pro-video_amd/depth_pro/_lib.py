@@ -20,8 +20,8 @@ DP_STORE_ROWS, DP_STORE_DECONV2X2, DP_STORE_HEAD_PS = 0, 1, 2
 (DP_TILE_AUTO, DP_TILE_128x128, DP_TILE_256x64, DP_TILE_256x32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x128,
  DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
- DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256) = range(17)
-DP_ABI_VERSION = 6
+ DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128) = range(18)
+DP_ABI_VERSION = 7
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -34,7 +34,7 @@ EXPORTS = (
     "dp_abi_version", "dp_gemm", "dp_layernorm", "dp_attention", "dp_attention_log2q", "dp_normalize_u8",
     "dp_resize_bilinear", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
     "dp_merge_windows_range", "dp_fov_tail", "dp_infer_epilogue", "dp_gemm_workspace_size", "dp_gemm_plan",
-    "dp_gemm_ln", "dp_depth_to_points",
+    "dp_depth_to_points", "dp_gemm_workspace_check",
 )
 
 
@@ -103,11 +103,11 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "dp_merge_windows": [vp, i32, i64, i32, i32, i32, vp, i32, vp],
         "dp_merge_windows_range": [vp, i32, i64, i32, i32, i32, i32, i32, vp, i32, vp],
         "dp_fov_tail": [vp, i32, vp, f32, vp, vp],
-        "dp_infer_epilogue": [vp, i32, i32, vp, i32, f64, i32, i32, vp, vp, vp],
+        "dp_infer_epilogue": [vp, i32, i32, vp, i32, f64, i32, i32, vp, vp, vp, vp],
         "dp_gemm_workspace_size": [],
+        "dp_gemm_workspace_check": [vp, vp, vp],
         "dp_depth_to_points": [vp, i32, i32, vp, f64, i32, vp, vp, vp, vp, vp],
         "dp_gemm_plan": [ctypes.POINTER(GemmArgs), ctypes.POINTER(i32), ctypes.POINTER(i32)],
-        "dp_gemm_ln": [ctypes.POINTER(GemmArgs), vp, vp, vp, i64, f32, i32, vp],
     }
     for name, argtypes in sig.items():
         fn = getattr(lib, name)

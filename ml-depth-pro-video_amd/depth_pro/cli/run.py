@@ -83,6 +83,11 @@ def run(args) -> int:
             continue
         pred = model.infer(transform(image), f_px=f_px)
         depth = pred["depth"].detach().cpu().numpy().squeeze()
+        try:
+            model.last_status().check()     # this frame's health, before anything is written
+        except Exception as e:
+            LOGGER.error(f"{image_path}: {e}")
+            continue
         if f_px is not None:
             LOGGER.debug(f"Focal length (from exif): {f_px:0.2f}")
         elif pred["focallength_px"] is not None:
@@ -100,21 +105,21 @@ def run(args) -> int:
             fig.canvas.draw()
             fig.canvas.flush_events()
         done += 1
-    model.engine().check_status(block=True)
     LOGGER.info("Done predicting depth!")
     if show:
         plt.show(block=True)
     return done
 
 
-def main(argv=None):
-    """`depth-pro-run` (reference :120-150)."""
+def main(argv=None) -> None:
+    """`depth-pro-run` (reference :120-150).  Returns None like the reference's main, so the console
+    script (`sys.exit(run_main())`) exits 0 on success; `run` returns the image count."""
     parser = argparse.ArgumentParser(description="Inference scripts of DepthPro with PyTorch models.")
     parser.add_argument("-i", "--image-path", type=Path, default="./data/example.jpg", help="Path to input image.")
     parser.add_argument("-o", "--output-path", type=Path, help="Path to store output files.")
     parser.add_argument("--skip-display", action="store_true", help="Skip matplotlib display.")
     parser.add_argument("-v", "--verbose", action="store_true", help="Show verbose output.")
-    return run(parser.parse_args(argv))
+    run(parser.parse_args(argv))
 
 
 if __name__ == "__main__":

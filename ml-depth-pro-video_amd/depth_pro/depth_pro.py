@@ -166,7 +166,10 @@ class DepthPro(nn.Module):
         output, e.g. received from rank 0 by `distributed.broadcast_packed`).  Its nn.Parameters
         live on the meta device: no checkpoint read, no fp32 copy in HBM."""
         m = cls(use_fov_head=use_fov_head, device=torch.device("meta"), compute_dtype=compute_dtype)
-        m._packed_device = torch.device(device)
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:   # 'cuda' -> the current device, as tensors get
+            device = torch.device("cuda", torch.cuda.current_device())
+        m._packed_device = device
         m._engine = Engine(packed, m._packed_device, compute_dtype, use_fov=use_fov_head)
         m.eval()
         return m
@@ -207,7 +210,16 @@ class DepthPro(nn.Module):
         """x3: (3, S, S) network-resolution frame on device -> engine outputs (static buffers)."""
         eng = self.engine()
         ops.resize_bilinear(x3, eng.x0)  # dtype conversion / copy into the static input
-        return eng.run()
+        out = eng.run()
+        eng.finish_status()
+        return out
+
+    def last_status(self):
+        """FrameStatus of the most recent frame this model ran (`engine.FrameStatus`): `.check()`
+        raises DPError if that frame's outputs are invalid (a timed-out stream-K hand-off, or NaN /
+        inf in depth or focal length) -- waiting for that frame only.  The frame loops call it
+        before writing a frame's files."""
+        return self.engine().last_status
 
     def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         """Canonical inverse depth (B,1,1536,1536) and FOV in degrees (B,1,1,1)."""
@@ -241,7 +253,7 @@ class DepthPro(nn.Module):
             x = x.unsqueeze(0)
         B, _, H, W = x.shape
         eng = self.engine()
-        if x.device != eng.dev:
+        if x.device.type != eng.dev.type or (x.device.index or 0) != eng.dev.index:
             raise DPError(f"input on {x.device}, model on {eng.dev}")
         if f_px is None and not self.use_fov_head:
             raise TypeError("f_px is required when the model has no FOV head")
@@ -254,10 +266,12 @@ class DepthPro(nn.Module):
             # prologue: (resize to) 1536^2 fp32 straight into the engine's static input
             ops.resize_bilinear(x[b], eng.x0)
             canonical, fov_deg = eng.run()
+            bad = eng.status_dev[-1:]     # NaN / inf outputs of this frame (FrameStatus)
             if f_px is None:
-                ops.infer_epilogue(canonical, fov_deg, None, H, W, depth[b], f_out[b])
+                ops.infer_epilogue(canonical, fov_deg, None, H, W, depth[b], f_out[b], bad)
             else:
-                ops.infer_epilogue(canonical, None, given, H, W, depth[b], None)
+                ops.infer_epilogue(canonical, None, given, H, W, depth[b], None, bad)
+            eng.finish_status()
         if f_px is None:
             f_px = f_out.squeeze()
         else:

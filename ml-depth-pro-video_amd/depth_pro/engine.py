@@ -221,30 +221,63 @@ class _ViTBuffers:
         self.out = self.h if out_dt == dt else self.a.view(out_dt)
 
 
-class _Rows:
-    """Rows [r0, r1) of a _ViTBuffers as contiguous views (one window group of the patch encoder)."""
+class FrameStatus:
+    """Health of ONE forward, read without stalling the stream that ran it.
 
-    def __init__(self, buf: _ViTBuffers, r0: int, r1: int):
-        self.rows = r1 - r0
-        for n in ("x", "h", "qkv", "a", "m", "out"):
-            setattr(self, n, getattr(buf, n)[r0:r1])
+    The forward ends with `dp_gemm_workspace_check` per GEMM workspace: the frame's error word
+    (a stream-K partial-tile hand-off that timed out) goes to the engine's status buffer and a set
+    word is cleared with every hand-off flag, so the next frame starts clean and reports only its
+    own launches.  `DepthPro.infer` adds a non-finite-output count from its epilogue kernel
+    (depth or focal length NaN / inf, e.g. an f16 overflow in the decoder), and
+    `Engine.finish_status` copies the words into pinned host memory on the same stream.
+    `check()` waits for that frame's copy only and raises DPError if the frame is bad, so a caller
+    that checks before writing a frame's files drops exactly the bad frame (generate_depth_maps,
+    depth-pro-run)."""
 
+    def __init__(self, frame: int, words: torch.Tensor, event: torch.cuda.Event):
+        self.frame = frame
+        self.words = words            # pinned int32: [workspace error words..., non-finite count]
+        self.event = event
 
-def window_groups(n: int):
-    """Split the 35 windows into n contiguous groups of near-equal size: [(w0, w1), ...]."""
-    n = max(1, min(int(n), NWIN))
-    cuts = [round(i * NWIN / n) for i in range(n + 1)]
-    return [(cuts[i], cuts[i + 1]) for i in range(n)]
+    def ready(self) -> bool:
+        return self.event.query()
+
+    def error(self) -> Optional[str]:
+        """None if the frame is good, else why not (synchronises on this frame's event)."""
+        self.event.synchronize()
+        w = self.words.tolist()
+        if any(w[:-1]):
+            return ("dp_gemm: a stream-K partial-tile hand-off timed out in this forward "
+                    "(workspace error word set): its depth map is invalid")
+        if w[-1]:
+            return f"{w[-1]} non-finite depth / focal-length value(s) in this frame's output"
+        return None
+
+    def check(self) -> None:
+        msg = self.error()
+        if msg is not None:
+            raise DPError(f"frame {self.frame}: {msg}")
 
 
 class Engine:
-    """One frame (batch 1) per forward; static workspace (~4 GB)."""
+    """One frame (batch 1) per forward; static workspace (~4 GB).
+
+    Streams (`_forward`): the main stream runs patchify -> patch encoder -> merges -> decoder ->
+    head; `side` runs the image encoder and `side2` the FOV encoder beside the patch encoder
+    (M = 577 rows each: far too few tiles to fill the chip alone); after the patch encoder the
+    project/upsample chains run on `dec_a` / `dec_b` and the decoder's encoder-feature projections,
+    the lat0 chain's last deconv and the FOV head on `dec_c`, beside the main stream's decoder.
+    At most four streams carry work at any time (HIP's default of four hardware queues per
+    process).  `serial_side = True` (profiling: bench.py's per-launch timing) issues everything
+    on the current stream in one order."""
 
     def __init__(self, packed: Dict[str, object], device: torch.device, dtype_code,
                  use_fov: bool = True):
         load()
         if device.type != "cuda":
             raise DPError("the MI355X Depth Pro engine needs a ROCm/HIP device")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         self.vcode, self.code = precision_codes(dtype_code)
         if packed[next(k for k in packed if k.endswith("attn.qkv.weight"))].dtype != ops.torch_dtype(self.vcode) \
                 or packed["decoder.convs.4"].dtype != ops.torch_dtype(self.code):
@@ -301,160 +334,88 @@ class Engine:
         self.f6 = e(6 * 6, 32)
         self.fov_deg = e(1, 1, 1, 1, dtype=torch.float32)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.side = torch.cuda.Stream(device=dev)
-        self.side2 = torch.cuda.Stream(device=dev)     # FOV encoder when DP_SIDE_STREAMS=2
-        # stream-K GEMM scratch, one per stream that issues GEMMs (main / side)
+        self.side = torch.cuda.Stream(device=dev)      # image encoder
+        self.side2 = torch.cuda.Stream(device=dev)     # FOV encoder
+        self.dec_a = torch.cuda.Stream(device=dev)     # lat0 project/upsample chain
+        self.dec_b = torch.cuda.Stream(device=dev)     # f1 / f0 / lat1 chains
+        self.dec_c = torch.cuda.Stream(device=dev)     # decoder projections, lat0's last deconv, FOV head
+        # stream-K GEMM scratch, one per stream that issues stream-K GEMMs (main / dec_c); the side
+        # encoders' and the dec_a / dec_b chains' GEMMs never take the stream-K engine (no
+        # workspace), so no two launches whose workgroups wait on each other run at once
         self.ws_main = ops.gemm_workspace(dev)
-        self.ws_side = ops.gemm_workspace(dev)
-        self.ws_side2 = ops.gemm_workspace(dev)
-        # project/upsample chains and the decoder's encoder-feature projections beside the main
-        # stream (DP_DEC_STREAMS=1, see _forward): two more streams, one of them issuing stream-K
-        self.dec_a = torch.cuda.Stream(device=dev)
-        self.dec_b = torch.cuda.Stream(device=dev)
-        self.dec_c = torch.cuda.Stream(device=dev)
         self.ws_dec = ops.gemm_workspace(dev)
-        self.dec_streams = os.environ.get("DP_DEC_STREAMS", "1") == "1"
-        self.small_conv_tile = int(os.environ.get("DP_SMALL_CONV_TILE", "0"))
-        self.conv768_tile = int(os.environ.get("DP_CONV768_TILE", "0"))
-        self.qkv_tile = int(os.environ.get("DP_QKV_TILE", "0"))   # A/B: patch-encoder qkv engine
-        self.side_sync = os.environ.get("DP_SIDE_SYNC", "0") == "1"
-        # decoder out_conv composed into the head's first conv (compose_head0); DP_HEAD0_COMPOSE=0: separate
+        # decoder out_conv composed into the head's first conv (compose_head0); DP_HEAD0_COMPOSE=0:
+        # separate (the per-stage parity test reads fusion 0's output on that path)
         self.head0_compose = os.environ.get("DP_HEAD0_COMPOSE", "1") == "1" and "head.0c.w" in packed
-        self.fov_at = int(os.environ.get("DP_FOV_AT", "-1"))
-        self.lat0_sk = os.environ.get("DP_LAT0_SK", "1") == "1"
-        # The 35 windows of the patch encoder are independent through all 24 blocks: run them as
-        # `DP_PATCH_GROUPS` window groups on their own streams, so one group's bandwidth-bound
-        # phases (LayerNorm, GEMM epilogues) overlap another group's MFMA phases.
-        self.set_patch_groups(int(os.environ.get("DP_PATCH_GROUPS", "1")), _init=True)
-        # their sticky error words (dp_mi355x.h DP_GEMM_WS_ERROR_OFFSET), read back asynchronously
-        # after every forward into pinned memory and checked by `check_status`
-        wss = [self.ws_main, self.ws_side, self.ws_side2, self.ws_dec] + self.ws_groups
-        self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32) for w in wss]
-        self._err_host = torch.zeros(len(wss), dtype=torch.int32, pin_memory=True)
-        self._err_ev: Optional[torch.cuda.Event] = None
-        self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
-        self.serial_side = False   # True: run the side encoders on the current stream (profiling)
-
-        # FOV encoder + head beside the decoder instead of the patch encoder (measured: 0.3 ms
-        # slower on MI355X, so off by default; DP_FOV_LATE=1 to try)
-        self.fov_late = os.environ.get("DP_FOV_LATE", "0") == "1"
-        # Measured and rejected: the side encoders' fc2 (M = 577, K = 4096, 24 workgroups) as 2 / 4
-        # accumulating K-slice launches, to shorten the workgroups that block the patch
-        # encoder's CUs: frame 24.32 -> 24.67 / 25.41 ms.
-        # where the image (+ FOV) encoders run (A/B switch, DP_SIDE_MODE):
-        #   concurrent -- side stream beside the patch encoder (default);
-        #   serial     -- main stream, ahead of the patch encoder;
-        #   late       -- side stream beside the project/upsample chain, after the patch encoder
-        self.side_mode = os.environ.get("DP_SIDE_MODE", "concurrent")
-        # the FOV encoder on a second side stream, joined only at the FOV head, so the join before
-        # fuse_lowres waits for the image encoder alone: 24.41-24.43 -> 24.16-24.25 ms per frame
-        # (DP_SIDE_STREAMS=1: both encoders on one side stream)
-        self.side_streams = int(os.environ.get("DP_SIDE_STREAMS", "2"))
-        # GEMM engine of the side encoders' block GEMMs (DP_SIDE_TILE, a DP_TILE_* value; 0 = planner)
-        self.side_tile = int(os.environ.get("DP_SIDE_TILE", "0"))
         # softmax scale * log2(e) folded into the qkv epilogue (per-column gamma on Q) so that attention
-        # takes one exp2 per score (dp_attention_log2q); DP_ATTN_LOG2Q=0: scale inside the attention
-        self.qkv_gamma = (ops.log2q_gamma(HEADS, D // HEADS, dev)
-                          if os.environ.get("DP_ATTN_LOG2Q", "1") == "1" else None)
-        # ViT LayerNorms fused into the patch encoder's proj / fc2 epilogues (dp_gemm_ln, DP_LN_FUSE=1).
-        # Measured and rejected (round 2, profiles/r02k_ln_fuse/): 40.35 / 40.44 fps fused vs 41.84 /
-        # 41.73 separate; eager proj + LN 100.6 us fused vs 67.8 + 22.5, fc2 + LN 194.2 vs 169.8 + 22.5:
-        # the row-band wait (every workgroup waits for the slowest of its band) and the normalise
-        # pass after it cost more than the LayerNorm pass they replace.
-        self.ln_fuse = os.environ.get("DP_LN_FUSE", "0") == "1"
-        if self.side_mode not in ("concurrent", "serial", "late"):
-            raise DPError(f"DP_SIDE_MODE={self.side_mode!r}")
+        # takes one exp2 per score (dp_attention_log2q)
+        self.qkv_gamma = ops.log2q_gamma(HEADS, D // HEADS, dev)
+        self.serial_side = False   # True: every launch on the current stream, in one order (profiling)
+        # device status of the current frame: [error word of each workspace (forward's end),
+        # non-finite output count (the infer epilogue)]
+        self._wss = [self.ws_main, self.ws_dec]
+        self.status_dev = torch.zeros(len(self._wss) + 1, dtype=torch.int32, device=dev)
+        self._frames = 0
+        self._recent: list = []           # FrameStatus of the last frames (check_status)
+        self.last_status: Optional[FrameStatus] = None
+        self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
 
     # ------------------------------------------------------------------ ViT
-    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, ln_fuse=False,
-             pre_fc1=None, pre_fc2=None):
-        for _ in self._vit_iter(pre, buf, n_img, cols_off_rows, hooks, ln_fuse, pre_fc1, pre_fc2):
-            pass
-
-    def _vit_iter(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, ln_fuse=False,
-                  pre_fc1=None, pre_fc2=None):
-        """The ViT as a generator: yields after each block (the side encoders step block by block
-        beside the patch encoder, DP_SIDE_SYNC); pre_fc1 / pre_fc2: callbacks before those GEMMs."""
+    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
+        """timm forward_features (vit_factory.py:97-99 -> vision_transformer.py): patch embed + cls /
+        pos, 24 Blocks, final norm; `hooks[i]()` runs after block i (encoder.py:133-144)."""
         P, M = self.P, n_img * TOK
-        # side encoders (one image, M = 577): engine choice for CU-time, not latency (DP_SIDE_TILE)
-        t = self.side_tile if n_img == 1 else 0
         # patch embed (k16 s16 conv as GEMM over the im2col rows) + bias + pos -> rows 1..576
         ops.gemm(self.cols, P[pre + "pe.w"], buf.x, M=n_img * PTOK, N=D, K=768,
                  A_off=cols_off_rows * 768, bias=P[pre + "pe.b"], pos=P[pre + "pos"], ldpos=D,
                  pos_group=PTOK, pos_off=1, row_group=PTOK, row_group_out=TOK, row_off=1)
         ops.vit_cls_rows(buf.x, P[pre + "cls"], P[pre + "pos"], n_img)
-        # LayerNorms fused into the residual GEMMs (dp_gemm_ln): norm2 rides on attn.proj, the
-        # next block's norm1 (or the final norm) on mlp.fc2; only block 0's norm1 -- after the
-        # patch embedding, whose cls rows come from another kernel -- is a pass of its own
-        # Its workgroups wait for the other workgroups of their row band, so two such launches
-        # must never run at once (each could hold CUs the other's missing workgroups need):
-        # only the patch encoder, alone on the main stream, uses it (ln_fuse), never the side
-        # encoders beside it nor concurrent window groups.
-        fuse = ln_fuse and self.ln_fuse and "ln" not in _ABLATE and "vitgemm" not in _ABLATE
+        ln, gemm = "ln" not in _ABLATE, "vitgemm" not in _ABLATE
         for i in range(DEPTH):
             b = f"{pre}blocks.{i}."
-            if "ln" not in _ABLATE and (i == 0 or not fuse):
+            if ln:
                 ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
-            if "vitgemm" not in _ABLATE:
+            if gemm:
                 ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"],
-                         gamma=self.qkv_gamma, tile=t or (self.qkv_tile if n_img > 1 else 0))
+                         gamma=self.qkv_gamma)
             if "attn" not in _ABLATE:
-                ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=self.qkv_gamma is not None)
-            ln2 = (P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, 1e-6) if fuse else None
-            if "vitgemm" not in _ABLATE:
+                ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
+            if gemm:
                 ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
-                         gamma=P[b + "ls1.gamma"], accumulate=True, tile=t, ln=ln2)
-            if "ln" not in _ABLATE and not fuse:
+                         gamma=P[b + "ls1.gamma"], accumulate=True)
+            if ln:
                 ops.layernorm(buf.x, P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, M, D)
-            nb = f"{pre}blocks.{i + 1}."
-            ln1 = None
-            if fuse:
-                ln1 = ((P[nb + "norm1.weight"], P[nb + "norm1.bias"], buf.h, 1e-6) if i + 1 < DEPTH else
-                       (P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, 1e-6))
-            if pre_fc1:
-                pre_fc1(i)
-            if "vitgemm" not in _ABLATE:
+            if gemm:
                 ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
-                         act=DP_ACT_GELU, tile=t)
-            if pre_fc2:
-                pre_fc2(i)
-            if "vitgemm" not in _ABLATE:
+                         act=DP_ACT_GELU)
                 ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
-                         gamma=P[b + "ls2.gamma"], accumulate=True, tile=t, ln=ln1)
+                         gamma=P[b + "ls2.gamma"], accumulate=True)
             if hooks and i in hooks:
                 hooks[i]()
-            yield i
-        if not fuse:
-            ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
+        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
-               stride=1, head_w=None, head_b=0.0, border_corr=None):
+               stride=1, border_corr=None):
         s_out = (s_in + 2 - 3) // stride + 1
-        # A/B (DP_SMALL_CONV_TILE, a DP_TILE_* value): engine of the decoder's small-grid
-        # ResidualBlock convs (48^2 / 96^2: 9 / 36 tiles of 256 x 256 on 256 CUs)
-        tile = self.small_conv_tile if (self.small_conv_tile and s_out <= 96 and cout == 256 and cin == 256) else 0
-        # A/B (DP_CONV768_TILE): engine of the 768^2 ResidualBlock convs (default: persistent 256 x 256)
-        if self.conv768_tile and s_out == 768 and cout == 256 and cin == 256:
-            tile = self.conv768_tile
         ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
                  conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
-                 relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout,
-                 head_w=head_w, head_b=head_b, ldc=cout, tile=tile, border_corr=border_corr)
+                 relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout, ldc=cout,
+                 border_corr=border_corr)
 
     def _deconv(self, x, s_in, cin, w, out, cout, bias=None, C_off=0, ldc=None):
         ops.gemm(x, w, out, M=s_in * s_in, N=4 * cout, K=cin, bias=bias, deconv=(s_in, s_in, cout),
                  C_off=C_off, ldc=cout if ldc is None else ldc)
 
     def _resblock(self, pre: str, x, s, out, extra=None):
-        """out = x (+ extra) + conv(relu(conv(relu(x)))) at s x s x 256."""
+        """out = x (+ extra) + conv(relu(conv(relu(x)))) at s x s x 256 (decoder.py:96-118)."""
         t = self.dec[s]["t"]
         P = self.P
         self._conv3(x, s, 256, P[pre + ".1.w"], t, 256, bias=P[pre + ".1.b"], relu_a=True, act=DP_ACT_RELU)
         self._conv3(t, s, 256, P[pre + ".3.w"], out, 256, bias=P[pre + ".3.b"], R1=x, R2=extra)
 
     def _fusion(self, i: int, feats, s, x1):
-        """FeatureFusionBlock2d i at resolution s (output at 2s for i != 0)."""
+        """FeatureFusionBlock2d i at resolution s (decoder.py:121-206; output at 2s for i != 0)."""
         P, d = self.P, self.dec[s]
         p = f"decoder.fusions.{i}."
         x = feats
@@ -471,57 +432,9 @@ class Engine:
         ops.gemm(d["y"], P[p + "out.w"], self.feats, M=s * s, N=256, K=256, bias=P[p + "out.b"])
         return self.feats
 
-    def set_patch_groups(self, n: int, _init: bool = False) -> None:
-        """Run the patch encoder as `n` concurrent window groups (drops a captured graph)."""
-        self.patch_groups = window_groups(n)
-        self.gstreams = [torch.cuda.Stream(device=self.dev) for _ in self.patch_groups[1:]]
-        self.ws_groups = [ops.gemm_workspace(self.dev) for _ in self.patch_groups[1:]]
-        if not _init:
-            self.graph = None
-            wss = [self.ws_main, self.ws_side, self.ws_side2, self.ws_dec] + self.ws_groups
-            self._err_dev = [w[ops.WS_ERROR_OFFSET:ops.WS_ERROR_OFFSET + 4].view(torch.int32) for w in wss]
-            self._err_host = torch.zeros(len(wss), dtype=torch.int32, pin_memory=True)
-            self._err_ev = None
-
-    def _patch_groups(self, main) -> None:
-        """The patch encoder as independent window groups, group g on stream g (group 0 on
-        `main`); each merges its own windows' share of the hooked block outputs."""
-        vp = self.vp
-        for g, (w0, w1) in enumerate(self.patch_groups):
-            serial = self.serial_side or g == 0
-            st = main if serial else self.gstreams[g - 1]
-            ws = self.ws_main if serial else self.ws_groups[g - 1]
-            if st is not main:
-                st.wait_stream(main)
-            lo, hi = min(w0, 25), min(w1, 25)   # their windows in the 5 x 5 hook grid
-            hooks = {}
-            if lo < hi:
-                hooks = {5: lambda lo=lo, hi=hi: ops.merge_windows(vp.x, 0, 5, 3, self.lat0, windows=(lo, hi)),
-                         11: lambda lo=lo, hi=hi: ops.merge_windows(vp.x, 0, 5, 3, self.lat1, windows=(lo, hi))}
-            with torch.cuda.stream(st), ops.use_workspace(ws):
-                self._vit("encoder.patch_encoder.", _Rows(vp, w0 * TOK, w1 * TOK), w1 - w0, w0 * PTOK, hooks)
-        if not self.serial_side:
-            for st in self.gstreams:
-                main.wait_stream(st)
-
-    # -------------------------------------------------------------- forward
-    def _image_encoder_iter(self):
-        """_image_encoder as a generator (one step per ViT block, the tail after the last)."""
-        P, e = self.P, "encoder."
-        yield from self._vit_iter("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
-        ops.merge_windows(self.vi.out, 0, 1, 0, self.g)
-        self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
-                     C_off=D, ldc=2 * D)
-
-    def _fov_encoder_iter(self):
-        vf, P = self.vf, self.P
-        yield from self._vit_iter("fov.encoder.0.", vf, 1, 34 * PTOK)
-        ops.gemm(vf.out, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
-
+    # -------------------------------------------------------------- encoders
     def _image_encoder(self):
-        """Image encoder (+ lowres upsample): ~2.5 % of the frame's FLOPs at M = 577
-        rows, far too few tiles to fill 256 CUs alone, so it runs on a side stream
-        beside the patch encoder."""
+        """Image encoder ViT on x2 (encoder.py:308-311) + the lowres upsample into `cat`."""
         P, e = self.P, "encoder."
         self._vit("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
         ops.merge_windows(self.vi.out, 0, 1, 0, self.g)
@@ -543,243 +456,121 @@ class Engine:
         self._conv3(self.f12, 12, 64, P["fov.h2.w"], self.f6, 32, bias=P["fov.h2.b"], act=DP_ACT_RELU, stride=2)
         ops.fov_tail(self.f6, P["fov.h4.w"], P["fov.h4.b"], self.fov_deg)
 
-    def forward(self, phase: str = "all") -> Tuple[torch.Tensor, torch.Tensor]:
-        """Run the network on `self.x0`; results in self.canonical / self.fov_deg.
-
-        `phase` splits the forward for the frame pipeline (depth_pro.pipeline): "side" = window
-        im2col + the image and FOV encoders, "enc" = the patch encoder, "dec" = everything after
-        it; the caller orders them (side before dec, enc before dec).  "all" = the whole frame."""
-        if phase not in ("all", "side", "enc", "dec"):
-            raise DPError(f"unknown forward phase {phase!r}")
+    # -------------------------------------------------------------- forward
+    def forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Run the network on `self.x0`; results in self.canonical / self.fov_deg.  Ends with the
+        workspace checks (part of a captured graph): status_dev[i] = workspace i's error word, and
+        a set word is cleared together with the hand-off flags, so the next forward starts clean."""
         with ops.use_workspace(self.ws_main):
-            return self._forward(phase)
+            out = self._forward()
+        for i, w in enumerate(self._wss):
+            ops.workspace_check(w, self.status_dev[i:i + 1])
+        return out
 
-    def _forward(self, phase: str = "all") -> Tuple[torch.Tensor, torch.Tensor]:
-        """Body of `forward`.
-
-        Two streams: the current stream runs the patch encoder -> decoder -> head;
-        `self.side` runs the image encoder beside the patch encoder (forked after
-        the window im2col, joined before fuse_lowres), then -- `fov_late` -- the
-        FOV encoder + FOV head beside the decoder (forked once the low-res
-        decoder features exist, joined at the end), so that only one M = 577
-        encoder competes with the patch encoder's full-chip GEMMs.
-        """
-        P = self.P
+    def _on(self, st: torch.cuda.Stream, after=None):
+        """Context: launches issued inside go to `st` (the current stream when serial) after `after`
+        (a stream or an event) has reached this point; GEMMs there take no stream-K engine unless
+        the caller sets a workspace inside."""
         main = torch.cuda.current_stream(self.dev)
-        side_ok = "side" not in _ABLATE
-        serial = self.serial_side or self.side_mode == "serial"
-        fov_side = self.use_fov and self.fov_late and not serial
-        if phase != "all" and (serial or fov_side or self.side_mode != "concurrent" or len(self.patch_groups) != 1):
-            raise DPError("forward phases need the default schedule (concurrent side encoders, one window group)")
-        if phase in ("all", "side"):
-            ops.patchify_pyramid(self.x0, self.cols)
-        if phase == "side":
-            # the image encoder on this stream, the FOV encoder on side2, joined before returning
-            with ops.use_workspace(self.ws_side):
-                self._image_encoder()
-            if self.use_fov:
-                self.side2.wait_stream(main)
-                with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
-                    self._fov_encoder()
-                main.wait_stream(self.side2)
-            return self.canonical, self.fov_deg
-
-        def side_encoders():
-            if serial:
-                self._image_encoder()
-                if self.use_fov:
-                    self._fov_encoder()
-                return
-            self.side.wait_stream(main)
-            with torch.cuda.stream(self.side), ops.use_workspace(self.ws_side):
-                if side_ok and "img" not in _ABLATE:
-                    self._image_encoder()
-                if side_ok:
-                    if self.use_fov and not fov_side and self.side_streams == 1:
-                        self._fov_encoder()
-            if self.use_fov and not fov_side and self.side_streams == 2 and fov_at < 0:
-                fov_encoder_side2()
-
-        def fov_encoder_side2():
-            self.side2.wait_stream(main)
-            with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
-                if side_ok and "fovenc" not in _ABLATE:
-                    self._fov_encoder()
-
-        # DP_FOV_AT=b (A/B): start the FOV encoder after patch-encoder block b instead of with the
-        # image encoder (it is needed only at the FOV head, after the decoder's first conv)
-        fov_at = self.fov_at if (self.use_fov and not fov_side and self.side_streams == 2 and not serial
-                                 and len(self.patch_groups) == 1) else -1
-        # DP_SIDE_SYNC (A/B): the side encoders step one block per patch-encoder block, each step
-        # beside that block's fc1 (multi-round, its last round leaves CUs free) and joined before
-        # its fc2, so they never hold CUs when a one-round proj / fc2 launches
-        sync = (self.side_sync and phase == "all" and not serial and not fov_side and self.side_mode == "concurrent"
-                and self.side_streams == 2 and self.use_fov and side_ok and fov_at < 0 and len(self.patch_groups) == 1)
-        side_its = None
-        if sync:
-            side_its = [(self.side, self.ws_side, self._image_encoder_iter()),
-                        (self.side2, self.ws_side2, self._fov_encoder_iter())]
-
-            def side_step(i):
-                for st, ws, it in side_its:
-                    st.wait_stream(main)
-                    with torch.cuda.stream(st), ops.use_workspace(ws):
-                        next(it)
-
-            def side_join(i):
-                main.wait_stream(self.side)
-                main.wait_stream(self.side2)
-        elif phase == "all" and (self.side_mode != "late" or serial):
-            side_encoders()
-        vp = self.vp
-        if phase == "dec":
-            pass
-        elif len(self.patch_groups) == 1:
-            hooks = {
-                5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
-                11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1),
-            }
-            if fov_at >= 0:
-                prev = hooks.get(fov_at)
-                hooks[fov_at] = (lambda: (prev(), fov_encoder_side2())) if prev else fov_encoder_side2
-            if sync:
-                self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True, pre_fc1=side_step,
-                          pre_fc2=side_join)
-                for st, ws, it in side_its:          # the side encoders' final norm and tails
-                    with torch.cuda.stream(st), ops.use_workspace(ws):
-                        for _ in it:
-                            pass
-            else:
-                self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks, ln_fuse=True)
+        if self.serial_side:
+            return ops.use_workspace(self.ws_main)
+        if isinstance(after, torch.cuda.Event):
+            st.wait_event(after)
         else:
-            self._patch_groups(main)
-        if phase != "dec":
-            ops.merge_windows(vp.out, 0, 5, 3, self.f0)
-            ops.merge_windows(vp.out, 25, 3, 6, self.f1)
-            ops.merge_windows(vp.out, 34, 1, 0, self.f2)
-        if phase == "enc":
-            return self.canonical, self.fov_deg
-        if self.side_mode == "late" and not serial:
-            side_encoders()
-        # project / upsample (encoder.py:314-324)
-        e = "encoder."
-        par = self.dec_streams and not serial and not fov_side
+            st.wait_stream(after if after is not None else main)
+        return _StreamCtx(st)
 
-        def lat0_pre():
+    def _forward(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        P, e = self.P, "encoder."
+        main = torch.cuda.current_stream(self.dev)
+        serial = self.serial_side
+        side_ok = "side" not in _ABLATE
+
+        def mark(st):
+            ev = torch.cuda.Event()
+            ev.record(main if serial else st)
+            return ev
+
+        # pyramid + 35 windows + patch-embed im2col (encoder.py:151-263)
+        ops.patchify_pyramid(self.x0, self.cols)
+        # image and FOV encoders beside the patch encoder (M = 577 rows each)
+        if side_ok:
+            with self._on(self.side):
+                if "img" not in _ABLATE:
+                    self._image_encoder()
+            if self.use_fov:
+                with self._on(self.side2):
+                    if "fovenc" not in _ABLATE:
+                        self._fov_encoder()
+        # patch encoder; hooks after blocks 5 / 11 (encoder.py:133-144, 267-288)
+        vp = self.vp
+        hooks = {5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
+                 11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1)}
+        self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks)
+        ops.merge_windows(vp.out, 0, 5, 3, self.f0)
+        ops.merge_windows(vp.out, 25, 3, 6, self.f1)
+        ops.merge_windows(vp.out, 34, 1, 0, self.f2)
+
+        # project / upsample (encoder.py:314-324): the latent and f0 / f1 chains (small grids) beside
+        # the main stream's f2 chain -> fuse_lowres -> convs.4, in the order the decoder's
+        # projections need their outputs
+        ev = {}
+        with self._on(self.dec_a):
             ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
             self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
             self._deconv(self.t192_256, 192, 256, P[e + "upsample_latent0.2"], self.t384_256, 256)
-
-        def lat0_last():   # 384^2 -> 768^2: 2304 tiles of K = 256, the stream-K engine's best case
-            self._deconv(self.t384_256, 384, 256, P[e + "upsample_latent0.3"], self.enc0, 256)
-
-        def lat0_chain():
-            lat0_pre()
-            lat0_last()
-
-        def lat1_chain():
+            ev["lat0pre"] = mark(self.dec_a)
+        with self._on(self.dec_b):
+            ops.gemm(self.f1, P[e + "upsample1.0"], self.t48_1024, M=48 * 48, N=D, K=D)
+            self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
+            ev["enc3"] = mark(self.dec_b)
+            ops.gemm(self.f0, P[e + "upsample0.0"], self.t96_512, M=96 * 96, N=512, K=D)
+            self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
+            ev["enc2"] = mark(self.dec_b)
             ops.gemm(self.lat1, P[e + "upsample_latent1.0"], self.t96_256b, M=96 * 96, N=256, K=D)
             self._deconv(self.t96_256b, 96, 256, P[e + "upsample_latent1.1"], self.t192_256b, 256)
             self._deconv(self.t192_256b, 192, 256, P[e + "upsample_latent1.2"], self.enc1, 256)
-
-        def f1_chain():
-            ops.gemm(self.f1, P[e + "upsample1.0"], self.t48_1024, M=48 * 48, N=D, K=D)
-            self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
-
-        def f0_chain():
-            ops.gemm(self.f0, P[e + "upsample0.0"], self.t96_512, M=96 * 96, N=512, K=D)
-            self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
-
-        enc_ev = {}
-        if par:
-            # The latent chains and the f0 / f1 chains (small grids, ~0.6 ms in a row) beside the
-            # main stream's f2 chain -> fuse_lowres -> convs.4, in the order the decoder's
-            # projections need their outputs (enc3, enc2, enc1; enc0 last).  Side streams issue no
-            # stream-K launch that could overlap one of the main stream's (workgroups that wait on
-            # each other, dp_mi355x.h): no workspace here.
-            lat0_sk = self.lat0_sk
-            for st, chains in ((self.dec_a, (("enc0pre", lat0_pre) if lat0_sk else ("enc0", lat0_chain),)),
-                               (self.dec_b, (("enc3", f1_chain), ("enc2", f0_chain), ("enc1", lat1_chain)))):
-                st.wait_stream(main)
-                with torch.cuda.stream(st), ops.use_workspace(None):
-                    for name, chain in chains:
-                        chain()
-                        enc_ev[name] = torch.cuda.Event()
-                        enc_ev[name].record(st)
-        else:
-            lat0_chain()
-            lat1_chain()
-            f0_chain()
-            f1_chain()
+            ev["enc1"] = mark(self.dec_b)
         ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
-        if not serial and phase == "all":
-            main.wait_stream(self.side)  # join: image-encoder half of `cat` and fov tokens ready
+        if not serial:
+            main.wait_stream(self.side)  # join: the image-encoder half of `cat`
         ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
         self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)
-        if par:
-            # FOV head (fov.py:56-82; needs only the low-res features) on the FOV encoder's stream,
-            # off the main stream's critical path (its 24^2 - 6^2 convs leave the chip idle)
-            if self.use_fov:
-                self.side2.wait_stream(main)
-                with torch.cuda.stream(self.side2), ops.use_workspace(self.ws_side2):
-                    self._fov_head()
-            # convs.3 / .2 / .1 (the encoder features' projections, decoder.py:74-93) on dec_c in
-            # the order the fusions need them, each beside the previous fusion block: after
-            # convs.4 (the main stream's last stream-K launch before fusion 1's deconv, which
-            # waits for convs.1), so dec_c's stream-K launches never overlap the main stream's
-            self.dec_c.wait_stream(main)
-            evs = {}
-            with torch.cuda.stream(self.dec_c), ops.use_workspace(self.ws_dec):
-                for i, (enc, s_, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)),
-                                          (1, (self.enc1, 384, 256))):
-                    self.dec_c.wait_event(enc_ev[f"enc{i}"])
-                    self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256)
-                    evs[i] = torch.cuda.Event()
-                    evs[i].record(self.dec_c)
-                # the lat0 chain's last deconv (on stream-K: 164 vs 446 us data-parallel) here, on the
-                # stream-K side stream; the main stream waits for it before fusion 1, whose deconv
-                # is its next stream-K launch
-                if lat0_sk:
-                    self.dec_c.wait_event(enc_ev["enc0pre"])
-                    lat0_last()
-                    enc_ev["enc0"] = torch.cuda.Event()
-                    enc_ev["enc0"].record(self.dec_c)
-        elif self.use_fov and not fov_side:  # FOV head (fov.py:56-82) only needs the lowres features
-            if self.side_streams == 2 and not serial and phase == "all":
-                main.wait_stream(self.side2)
-            self._fov_head()
-        elif fov_side:
-            self.side.wait_stream(main)
-            with torch.cuda.stream(self.side), ops.use_workspace(self.ws_side):
-                if side_ok:
-                    self._fov_encoder()
-                    self._fov_head()
+        # dec_c (after convs.4, the main stream's last stream-K launch before fusion 1's deconv, which
+        # waits for convs.1 -- so dec_c's stream-K launches never overlap the main stream's):
+        # convs.3 / .2 / .1 in the order the fusions need them, the lat0 chain's 384^2 -> 768^2
+        # deconv (stream-K), then the FOV head (needs only the low-res features and the FOV tokens)
+        with self._on(self.dec_c), ops.use_workspace(self.ws_main if serial else self.ws_dec):
+            for i, (enc, s_, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)),
+                                      (1, (self.enc1, 384, 256))):
+                if not serial:
+                    self.dec_c.wait_event(ev[f"enc{i}"])
+                self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256)
+                ev[f"c{i}"] = mark(self.dec_c)
+            if not serial:
+                self.dec_c.wait_event(ev["lat0pre"])
+            self._deconv(self.t384_256, 384, 256, P[e + "upsample_latent0.3"], self.enc0, 256)
+            ev["enc0"] = mark(self.dec_c)
+            if self.use_fov and side_ok:
+                if not serial:
+                    self.dec_c.wait_stream(self.side2)
+                self._fov_head()
         if "decoder" not in _ABLATE:
             f = self._fusion(4, self.low, 48, None)
-            for i, (enc, s, cin) in ((3, (self.enc3, 96, D)), (2, (self.enc2, 192, 512)), (1, (self.enc1, 384, 256))):
-                c = self.dec[s]["c"]
-                if par:
-                    main.wait_event(evs[i])
+            for i, s in ((3, 96), (2, 192), (1, 384)):
+                if not serial:
+                    main.wait_event(ev[f"c{i}"])
                     if i == 1:
-                        main.wait_event(enc_ev["enc0"])
-                else:
-                    self._conv3(enc, s, cin, P[f"decoder.convs.{i}"], c, 256)
-                f = self._fusion(i, f, s, c)
-            if par:
-                main.wait_event(enc_ev["enc0"])     # lat0 chain for fusion 0
+                        main.wait_event(ev["enc0"])
+                f = self._fusion(i, f, s, self.dec[s]["c"])
             feats = self._fusion(0, f, 768, self.enc0)
         else:
             feats = self.feats
-        if par:
-            main.wait_stream(self.dec_a)
-            main.wait_stream(self.dec_b)
-            main.wait_stream(self.dec_c)
-            if self.use_fov:
-                main.wait_stream(self.side2)
-        if fov_side:
-            main.wait_stream(self.side)
+        if not serial:
+            for st in (self.dec_a, self.dec_b, self.dec_c, self.side2):
+                main.wait_stream(st)
         if "head" in _ABLATE:
             return self.canonical, self.fov_deg
         # head (depth_pro.py:182-207): conv3x3, then deconv -> conv3x3 -> ReLU -> 1x1 -> ReLU as ONE
@@ -808,39 +599,50 @@ class Engine:
         self.graph = g
 
     def run(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        """One forward (graph replay if captured).  Raises DPError if an EARLIER forward's
-        stream-K hand-off timed out (or this one's, with DP_CHECK_SYNC=1)."""
-        self.check_status(block=False)
+        """One forward (graph replay if captured) on the current stream.  Its health lands in
+        `status_dev`; `finish_status` (after whatever else writes it, e.g. the infer epilogue's
+        non-finite count) turns it into this frame's FrameStatus."""
         if self.graph is not None:
             self.graph.replay()
         else:
             self.forward()
-        self._stage_status()
-        if self.sync_check:
-            self.check_status(block=True)
         return self.canonical, self.fov_deg
 
-    def _stage_status(self) -> None:
-        for i, w in enumerate(self._err_dev):
-            self._err_host[i:i + 1].copy_(w, non_blocking=True)
-        self._err_ev = torch.cuda.Event()
-        self._err_ev.record()
+    def finish_status(self) -> FrameStatus:
+        """Snapshot this frame's status words into pinned memory (asynchronously, on the current
+        stream), reset the non-finite counter for the next frame, and return the FrameStatus."""
+        words = torch.empty(self.status_dev.numel(), dtype=torch.int32, pin_memory=True)
+        words.copy_(self.status_dev, non_blocking=True)
+        self.status_dev[-1:].zero_()
+        ev = torch.cuda.Event()
+        ev.record()
+        st = FrameStatus(self._frames, words, ev)
+        self._frames += 1
+        self._recent = (self._recent + [st])[-64:]
+        self.last_status = st
+        if self.sync_check:
+            st.check()
+        return st
 
     def check_status(self, block: bool = True) -> None:
-        """Raise DPError if a stream-K GEMM of a forward run so far gave up waiting for a
-        partial tile (its output -- that frame's depth -- is wrong).  block=False only looks
-        at read-backs that have already landed (no synchronisation)."""
-        ev = self._err_ev
-        if ev is None:
-            return
-        if block:
-            ev.synchronize()
-        elif not ev.query():
-            return
-        self._err_ev = None
-        if int(self._err_host.abs().sum()) != 0:
-            self._err_host.zero_()
-            for w in [self.ws_main, self.ws_side, self.ws_side2, self.ws_dec] + self.ws_groups:
-                w.zero_()   # error word, and any hand-off flag the timed-out launch left set
-            raise DPError("dp_gemm: a stream-K partial-tile or fused-LayerNorm row-band hand-off timed out; "
-                          "the depth map of a recent frame is invalid (workspace error word set)")
+        """Raise DPError if one of the recent frames is bad (block=False: only frames already done)."""
+        for st in self._recent:
+            if block or st.ready():
+                st.check()
+
+
+class _StreamCtx:
+    """torch.cuda.stream(st) + no stream-K workspace for the GEMMs issued inside."""
+
+    def __init__(self, st):
+        self.st = torch.cuda.stream(st)
+        self.ws = ops.use_workspace(None)
+
+    def __enter__(self):
+        self.st.__enter__()
+        self.ws.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self.ws.__exit__(*exc)
+        return self.st.__exit__(*exc)

@@ -95,6 +95,13 @@ def workspace_error(ws: torch.Tensor) -> int:
     return int(ws[WS_ERROR_OFFSET:WS_ERROR_OFFSET + 4].view(torch.int32).item())
 
 
+def workspace_check(ws: torch.Tensor, status: torch.Tensor) -> None:
+    """dp_gemm_workspace_check: status (device int32, one element) = the sticky error word of `ws`;
+    a set word is cleared with every hand-off flag (stream-ordered, graph-capturable)."""
+    check(_lib.load().dp_gemm_workspace_check(ws.data_ptr(), status.data_ptr(), _stream(status)),
+          "dp_gemm_workspace_check")
+
+
 def gemm_workspace(device: torch.device) -> torch.Tensor:
     """A zeroed device buffer of dp_gemm_workspace_size() bytes."""
     return torch.zeros(int(_lib.load().dp_gemm_workspace_size()), dtype=torch.uint8, device=device)
@@ -135,14 +142,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          head_corr: Optional[torch.Tensor] = None,
          A_off: int = 0, C_off: int = 0, B_off: int = 0, tile: int = 0,
          workspace: Optional[torch.Tensor] = None,
-         plan_only: bool = False, ln: Optional[tuple] = None, border_corr: Optional[torch.Tensor] = None):
+         plan_only: bool = False, border_corr: Optional[torch.Tensor] = None):
     """dp_gemm. `A_off`/`B_off`/`C_off` are element offsets into A / B / C (sub-views, e.g. a
     K slice of a split-K GEMM: A_off = B_off = k0 with lda / ldb the full row lengths).
 
     `workspace` (or the one set by `use_workspace`) enables the stream-K engine.
     `plan_only=True` launches nothing and returns (tile, workgroups) from dp_gemm_plan.
-    `ln=(w, b, out, eps)`: dp_gemm_ln -- also write LayerNorm(C rows) * w + b to the 16-bit
-    `out` (fused into the epilogue where the launch allows it).
     """
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
@@ -194,14 +199,6 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
         check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
         return t.value, g.value
     _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None, B_off)
-    if ln is not None:
-        w, b, out, eps = ln
-        if out.numel() < (M - 1) * N + N or w.numel() < N or b.numel() < N:
-            raise _lib.DPError("dp_gemm_ln: LayerNorm output / affine tensors too small")
-        with _Timed("gemm_ln", 2.0 * M * N * K, (M, N, K), B.dtype):
-            check(_lib.load().dp_gemm_ln(ctypes.byref(a), w.data_ptr(), b.data_ptr(), out.data_ptr(), N, float(eps),
-                                         dtype_code(out.dtype), _stream(C)), "dp_gemm_ln")
-        return
     kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
     with _Timed(kind, 2.0 * M * N * K, (M, N, K), B.dtype):
         check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
@@ -308,9 +305,11 @@ def fov_tail(x6: torch.Tensor, w: torch.Tensor, bias: float, out: torch.Tensor) 
 
 
 def infer_epilogue(canonical: torch.Tensor, fov_deg: Optional[torch.Tensor], f_given: Optional[float],
-                   H: int, W: int, depth: torch.Tensor, f_px_out: Optional[torch.Tensor]) -> None:
+                   H: int, W: int, depth: torch.Tensor, f_px_out: Optional[torch.Tensor],
+                   nonfinite: Optional[torch.Tensor] = None) -> None:
+    """dp_infer_epilogue; `nonfinite` (device int32, optional) counts NaN / inf outputs."""
     SH, SW = canonical.shape[-2:]
     use_given = f_given is not None
     check(_lib.load().dp_infer_epilogue(canonical.data_ptr(), SH, SW, _p(fov_deg), int(use_given),
                                         float(f_given) if use_given else 0.0, H, W, depth.data_ptr(),
-                                        _p(f_px_out), _stream(depth)), "dp_infer_epilogue")
+                                        _p(f_px_out), _p(nonfinite), _stream(depth)), "dp_infer_epilogue")

@@ -209,6 +209,19 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
 
     successful = 0
     t0 = time.time()
+    # frames queued to the writers but not written yet (each holds pinned host copies of its
+    # depth map and, with --pointcloud, its points): at most this many, so host memory stays
+    # bounded when PNG / PLY writing falls behind the GPU
+    max_inflight = 2 * encode_workers
+
+    def collect(f):
+        nonlocal successful
+        try:
+            if f is not None and f.result() is not None:
+                successful += 1
+        except Exception as e:  # a bad frame or a write failure skips that frame, like the reference
+            print(f"Error writing a depth map: {e}")
+
     with ThreadPoolExecutor(decode_workers) as dec, ThreadPoolExecutor(encode_workers) as enc:
         futs = {k: dec.submit(_load, image_paths[k], downscale_factor) for k in mine[: 2 * decode_workers]}
         nxt = 2 * decode_workers
@@ -216,6 +229,8 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
         for n, k in enumerate(mine):
             base_name = os.path.splitext(os.path.basename(image_paths[k]))[0]
             output_path = os.path.join(output_dir, output_name(image_paths[k]))
+            while len(pending) >= max_inflight:
+                collect(pending.pop(0))
             try:
                 image, f_px = futs.pop(k).result()
                 if nxt < len(mine):
@@ -224,9 +239,13 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 with torch.no_grad():
                     pred = model.infer(transform(image), f_px=f_px)
                     depth = pred["depth"]
+                # this frame's health (engine.FrameStatus: a timed-out stream-K hand-off, NaN / inf
+                # output), checked by the writer after the frame's event, before any file is written
+                status = model.last_status() if hasattr(model, "last_status") else None
                 pc = None
                 if depth.is_cuda:
-                    # queue every device->host copy behind the frame; a writer thread waits on its event
+                    # queue every device->host copy behind the frame on this stream; a writer thread
+                    # waits on its event
                     host = torch.empty(depth.shape, dtype=depth.dtype, pin_memory=True)
                     host.copy_(depth, non_blocking=True)
                     if pointcloud:
@@ -236,9 +255,11 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 else:
                     host, ev = depth, None
 
-                def _finish(host=host, ev=ev, path=output_path, pc=pc, base=base_name):
+                def _finish(host=host, ev=ev, path=output_path, pc=pc, base=base_name, status=status):
                     if ev is not None:
                         ev.synchronize()
+                    if status is not None:
+                        status.check()          # raises: this frame is dropped, nothing written
                     if pc is not None:
                         PC.write_ply(os.path.join(output_dir, f"{base}_points.ply"), *_points_host(pc))
                     return _encode(host.numpy(), path, colored, cmap)
@@ -249,13 +270,7 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 pending.append(None)
             print(f"[{n + 1}/{len(mine)}] Processing {base_name}")
         for f in pending:
-            try:
-                if f is not None and f.result() is not None:
-                    successful += 1
-            except Exception as e:  # an encode / write failure skips that frame, like the reference
-                print(f"Error writing a depth map: {e}")
-    if hasattr(model, "engine"):
-        model.engine().check_status(block=True)
+            collect(f)
     dt = time.time() - t0
     print(f"Processing complete: {successful}/{len(mine)} images successfully processed "
           f"({len(mine) / max(dt, 1e-9):.2f} frames/s on rank {rank})")
@@ -264,20 +279,24 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
 
 def _points(depth: torch.Tensor, f_px, image: np.ndarray):
     """Queue the frame's point cloud on the GPU (depth_to_3d, img_to_normalized_pointcloud.py:819-856)
-    without a host synchronisation: full-size buffers + the device point count."""
+    and its copy into pinned host buffers, on the current stream, without a host synchronisation:
+    full-size buffers + the point count (the writer slices them after the frame's event)."""
     h, w = depth.shape
     rgb = torch.from_numpy(np.ascontiguousarray(image)).to(depth.device, non_blocking=True)
     xyz, _, cols, count = PC.depth_to_points_async(depth, f_px, w, h, rgb=rgb)
-    n_host = torch.empty((), dtype=torch.int32, pin_memory=True)
-    n_host.copy_(count, non_blocking=True)
-    return xyz, cols, n_host
+    out = []
+    for t in (xyz, cols, count):
+        hbuf = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        hbuf.copy_(t, non_blocking=True)
+        out.append(hbuf)
+    return tuple(out)
 
 
 def _points_host(pc):
-    """Writer-thread side (after the frame's event): copy back exactly the valid points."""
+    """Writer-thread side (after the frame's event): exactly the valid points."""
     xyz, cols, n_host = pc
     n = int(n_host)
-    return xyz[:n].cpu().numpy(), cols[:n].cpu().numpy()
+    return xyz[:n].numpy(), cols[:n].numpy()
 
 
 def main():

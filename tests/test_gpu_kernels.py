@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 from depth_pro import ops  # noqa: E402
 from depth_pro._lib import (DP_ACT_GELU, DP_ACT_RELU, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa: E402
                             DP_TILE_BIG_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_512x128,
-                            DP_TILE_STREAMK_256x256)
+                            DP_TILE_DUAL_256x128, DP_TILE_STREAMK_256x256)
 
 DTYPES = [torch.bfloat16, torch.float16]
 
@@ -257,7 +257,7 @@ def test_normalize_u8(cuda):
 
 
 TILES = {"128x128": 1, "256x64": 2, "256x32": 3, "big256x256": 4, "big256x128": 5, "big256x256k32": 6,
-         "big256x128k32": 7, "8ph256x256": 8}
+         "big256x128k32": 7, "8ph256x256": 8, "dual256x128": 17}
 
 
 @pytest.mark.parametrize("tile", list(TILES))
@@ -348,7 +348,7 @@ def test_gemm_stream_k_conv3x3_relu_residual(cuda, dt):
 
 
 ENGINES = [DP_TILE_BIG_256x256, DP_TILE_8PH_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_256x128, DP_TILE_BIG_512x128,
-           DP_TILE_STREAMK_256x256]
+           DP_TILE_STREAMK_256x256, DP_TILE_DUAL_256x128]
 
 
 @pytest.mark.parametrize("tile", ENGINES)
@@ -473,141 +473,6 @@ def test_persistent_engine_bit_identical_to_data_parallel(cuda, dt, pair, case):
     assert torch.equal(C1, C2), (C1.float() - C2.float()).abs().max().item()
 
 
-@pytest.mark.parametrize("pair", ["320", "256"])
-@pytest.mark.parametrize("case", ["dense_bias", "gelu_ragged", "acc_f32"])
-def test_persistent_engine_tile_queues(cuda, pair, case):
-    """With a workspace the persistent engine draws its tiles from the per-XCD ticket queues
-    (dp_gemm.hip tq_draw): bit-identical to the data-parallel engine, every counter back at
-    zero after each launch (last workgroup resets them), also for back-to-back launches,
-    under HIP-graph replay, and beside a concurrent GEMM on another stream that holds CUs
-    while the persistent grid starts (late workgroups take fewer tiles)."""
-    from depth_pro._lib import DP_TILE_PBIG_256x256, DP_TILE_PBIG_320x256
-
-    dt = torch.bfloat16
-    tp, tb = (DP_TILE_PBIG_320x256, DP_TILE_BIG_320x256) if pair == "320" else (DP_TILE_PBIG_256x256,
-                                                                                  DP_TILE_BIG_256x256)
-    g = torch.Generator().manual_seed(11 + sum(map(ord, case)))
-    M, N, K = {"dense_bias": (20195, 3072, 1024), "gelu_ragged": (4999, 1536, 512),
-               "acc_f32": (3001, 1024, 2048)}[case]
-    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
-    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
-    kw = dict(bias=torch.randn(N, generator=g).to(cuda))
-    if case == "gelu_ragged":
-        kw.update(act=DP_ACT_GELU)
-    if case == "acc_f32":
-        kw.update(gamma=torch.rand(N, generator=g).to(cuda), accumulate=True)
-        C0 = torch.randn(M, N, generator=g).to(cuda)
-    else:
-        C0 = torch.full((M, N), 7.0, dtype=dt, device=cuda)
-    ws = ops.gemm_workspace(cuda)
-    q = ws[2048:3200].view(torch.int32)
-    ref = C0.clone()
-    ops.gemm(A, B, ref, M=M, N=N, K=K, tile=tb, **kw)
-    for _ in range(3):                                  # back to back: counters reset in between
-        C = C0.clone()
-        ops.gemm(A, B, C, M=M, N=N, K=K, tile=tp, workspace=ws, **kw)
-        torch.cuda.synchronize()
-        assert torch.equal(C, ref), (C.float() - ref.float()).abs().max().item()
-        assert int(q.abs().sum()) == 0, q.nonzero()
-    # beside a long GEMM on another stream (its own workspace)
-    side = torch.cuda.Stream(device=cuda)
-    ws2 = ops.gemm_workspace(cuda)
-    A2 = rnd(8192, 4096, dt=dt, dev=cuda, gen=g)
-    B2 = rnd(4096, 4096, dt=dt, dev=cuda, gen=g, scale=4096 ** -0.5)
-    C2 = torch.empty(8192, 4096, dtype=dt, device=cuda)
-    C = C0.clone()
-    side.wait_stream(torch.cuda.current_stream(cuda))
-    with torch.cuda.stream(side):
-        ops.gemm(A2, B2, C2, M=8192, N=4096, K=4096, workspace=ws2)
-    ops.gemm(A, B, C, M=M, N=N, K=K, tile=tp, workspace=ws, **kw)
-    torch.cuda.synchronize()
-    assert torch.equal(C, ref)
-    assert int(q.abs().sum()) == 0
-    # graph replay
-    C = C0.clone()
-    gr = torch.cuda.CUDAGraph()
-    s = torch.cuda.Stream(device=cuda)
-    s.wait_stream(torch.cuda.current_stream(cuda))
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(gr, stream=s):
-            ops.gemm(A, B, C, M=M, N=N, K=K, tile=tp, workspace=ws, **kw)
-    torch.cuda.current_stream(cuda).wait_stream(s)
-    for _ in range(2):
-        if case == "acc_f32":
-            C.copy_(C0)
-        gr.replay()
-        torch.cuda.synchronize()
-        assert torch.equal(C, ref)
-        assert int(q.abs().sum()) == 0
-
-
-@pytest.mark.parametrize("case", ["patch_proj", "patch_fc2", "side_fc2", "ragged", "unfused_big", "f16_out",
-                                  "forced_unfused"])
-def test_gemm_residual_layernorm(cuda, case):
-    """dp_gemm_ln: the residual-accumulate GEMM (timm Block: x += ls * (h W^T + b)) and the next
-    LayerNorm of the new rows.  C is bit-identical to dp_gemm; the LN rows match an fp32 torch
-    LayerNorm of that C to the 16-bit rounding of the output (the fused epilogue combines
-    per-wave (mean, M2) partials exactly, only the fp32 summation order differs); the row-band
-    counters are back at zero after every launch and under graph replay.  Shapes: the patch
-    encoder's proj / fc2 (M = 20195, one round of 256 workgroups on the 320x256 engine), a side
-    encoder's fc2 (M = 577, 256x128 engine), a ragged M, a grid too large to fuse (GEMM + LN
-    pass), an f16 LN output, and the unfused path forced by debug bit 65536."""
-    from depth_pro import _lib
-
-    M, K, odt = {"patch_proj": (20195, 1024, torch.bfloat16), "patch_fc2": (20195, 4096, torch.bfloat16),
-                 "side_fc2": (577, 4096, torch.bfloat16), "ragged": (3001, 2048, torch.bfloat16),
-                 "unfused_big": (40000, 1024, torch.bfloat16), "f16_out": (577, 1024, torch.float16),
-                 "forced_unfused": (20195, 1024, torch.bfloat16)}[case]
-    N, dt = 1024, torch.bfloat16
-    g = torch.Generator().manual_seed(sum(map(ord, case)))
-    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
-    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
-    kw = dict(bias=torch.randn(N, generator=g).to(cuda), gamma=torch.rand(N, generator=g).to(cuda), accumulate=True)
-    # a residual stream with a per-row offset and a few large channels (mean far from 0)
-    x0 = (torch.randn(M, N, generator=g) * 2 + torch.randn(M, 1, generator=g) * 5).to(cuda)
-    x0[:, 7] += 40.0
-    w = (1 + 0.1 * torch.randn(N, generator=g)).to(cuda)
-    b = (0.1 * torch.randn(N, generator=g)).to(cuda)
-    ws = ops.gemm_workspace(cuda)
-    cnt = ws[3200:4088].view(torch.int32)
-    ref = x0.clone()
-    ops.gemm(A, B, ref, M=M, N=N, K=K, workspace=ws, **kw)
-    lref = F.layer_norm(ref, (N,), w, b, eps=1e-6)
-    lib = _lib.load()
-    if case == "forced_unfused":
-        lib.dp_gemm_debug_flags(65536)
-    try:
-        for _ in range(2):
-            C = x0.clone()
-            y = torch.full((M, N), float("nan"), dtype=odt, device=cuda)
-            ops.gemm(A, B, C, M=M, N=N, K=K, workspace=ws, ln=(w, b, y, 1e-6), **kw)
-            torch.cuda.synchronize()
-            assert torch.equal(C, ref)
-            err = (y.float() - lref).abs()
-            tol = lref.abs() * (2.0 ** -8 if odt == torch.bfloat16 else 2.0 ** -11) + 1e-4
-            assert bool((err <= tol).all()), (err - tol).max().item()
-            assert int(cnt.abs().sum()) == 0 and ops.workspace_error(ws) == 0
-    finally:
-        lib.dp_gemm_debug_flags(0)
-    if case == "patch_fc2":   # graph replay of the fused launch
-        C = x0.clone()
-        y = torch.empty(M, N, dtype=odt, device=cuda)
-        gr = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(device=cuda)
-        s.wait_stream(torch.cuda.current_stream(cuda))
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(gr, stream=s):
-                ops.gemm(A, B, C, M=M, N=N, K=K, workspace=ws, ln=(w, b, y, 1e-6), **kw)
-        torch.cuda.current_stream(cuda).wait_stream(s)
-        for _ in range(2):
-            C.copy_(x0)
-            gr.replay()
-            torch.cuda.synchronize()
-            assert torch.equal(C, ref)
-            assert bool(((y.float() - lref).abs() <= lref.abs() * 2.0 ** -8 + 1e-4).all())
-            assert int(cnt.abs().sum()) == 0 and ops.workspace_error(ws) == 0
-
-
 @pytest.mark.parametrize("dt", DTYPES)
 def test_conv3x3_border_corrected_composition(cuda, dt):
     """dp_gemm DP_STORE_ROWS with head_corr (the decoder out_conv composed into head.0,
@@ -631,3 +496,57 @@ def test_conv3x3_border_corrected_composition(cuda, dt):
              conv=dict(in_h=S, in_w=S, in_c=c, k=3, stride=1, pad=1, out_h=S, out_w=S),
              bias=P["head.0c.b"], border_corr=P["head.0c.corr"], tile=DP_TILE_BIG_512x128)
     close(out, ref, dt, "border-corrected composed conv")
+
+
+def test_border_correction_rejects_relu_prologue(cuda):
+    """head_corr (composed-conv border correction) exists only in the non-ReLU 512x128 conv
+    instantiation: a ReLU-on-load request must be refused on the host, not run uncorrected."""
+    from depth_pro._lib import DPError
+
+    S, c, o = 32, 128, 128
+    x = torch.zeros(S * S, c, dtype=torch.float16, device=cuda)
+    w = torch.zeros(o, 9 * c, dtype=torch.float16, device=cuda)
+    out = torch.empty(S * S, o, dtype=torch.float16, device=cuda)
+    corr = torch.zeros(9 * o, device=cuda)
+    kw = dict(M=S * S, N=o, K=9 * c, conv=dict(in_h=S, in_w=S, in_c=c, k=3, stride=1, pad=1, out_h=S, out_w=S),
+              border_corr=corr, tile=DP_TILE_BIG_512x128)
+    ops.gemm(x, w, out, **kw)                              # accepted without the ReLU prologue
+    with pytest.raises(DPError, match="DP_ERR_ARG"):
+        ops.gemm(x, w, out, relu_a=True, **kw)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_fov_tail_vs_conv2d(cuda, dt):
+    """dp_fov_tail (fov.py:46, head[4]: Conv2d(32, 1, 6) + bias on the 6x6x32 map) vs F.conv2d."""
+    g = torch.Generator().manual_seed(46)
+    x = torch.randn(1, 32, 6, 6, generator=g).to(dt)
+    w = torch.randn(1, 32, 6, 6, generator=g) * 0.1
+    b = 0.37
+    x6 = x[0].permute(1, 2, 0).contiguous().to(cuda)      # NHWC 6x6x32
+    out = torch.empty(1, 1, 1, 1, device=cuda)
+    ops.fov_tail(x6, w.reshape(-1).contiguous().to(cuda), b, out)
+    ref = F.conv2d(x.float(), w, torch.tensor([b]))
+    assert abs(out.item() - ref.item()) <= 1e-5 * max(1.0, abs(ref.item())), (out.item(), ref.item())
+
+
+def test_infer_epilogue_counts_nonfinite_and_keeps_nan(cuda):
+    """dp_infer_epilogue's health word: NaN / inf depth values are counted (and a NaN stays NaN,
+    as torch.clamp does), a finite map counts nothing; a NaN FOV (hence f_px) counts too."""
+    canon = torch.rand(1, 1, 1536, 1536, device=cuda) + 0.5
+    fov = torch.full((1, 1, 1, 1), 60.0, device=cuda)
+    bad = torch.zeros(1, dtype=torch.int32, device=cuda)
+    depth = torch.empty(1536, 1536, device=cuda)
+    fpx = torch.empty((), device=cuda)
+    ops.infer_epilogue(canon, fov, None, 1536, 1536, depth, fpx, bad)
+    assert int(bad) == 0
+    canon[0, 0, 5, 7] = float("nan")
+    canon[0, 0, 900, 11] = float("nan")
+    ops.infer_epilogue(canon, fov, None, 1536, 1536, depth, fpx, bad)
+    assert int(bad) == 2 and torch.isnan(depth[5, 7]) and torch.isnan(depth[900, 11])
+    ref = 1.0 / torch.clamp(canon * (1536 / fpx), 1e-4, 1e4)
+    assert torch.equal(torch.isnan(depth), torch.isnan(ref[0, 0]))
+    bad.zero_()
+    canon[0, 0, 5, 7] = 1.0
+    canon[0, 0, 900, 11] = 1.0
+    ops.infer_epilogue(canon, torch.full_like(fov, float("nan")), None, 1536, 1536, depth, fpx, bad)
+    assert int(bad) == 1 + 1536 * 1536       # f_px and every depth value

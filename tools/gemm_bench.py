@@ -11,14 +11,15 @@ from depth_pro._lib import (DP_TILE_128x128, DP_TILE_256x64, DP_TILE_8PH_256x256
                             DP_TILE_BIG_256x128_K32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32,
                             DP_TILE_DEEP4_256x256, DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128,
                             DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_512x128,
-                            DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256)
+                            DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128)
 
 TILES = (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
          ("8ph256x256", DP_TILE_8PH_256x256), ("deep4_256x256", DP_TILE_DEEP4_256x256),
          ("deep5_256x256", DP_TILE_DEEP5_256x256), ("deep6_256x128", DP_TILE_DEEP_256x128),
          ("sk256x256", DP_TILE_STREAMK_256x256), ("big320x256", DP_TILE_BIG_320x256),
          ("small128x128", DP_TILE_128x128), ("big512x128", DP_TILE_BIG_512x128), ("small256x64", DP_TILE_256x64),
-         ("pbig320x256", DP_TILE_PBIG_320x256), ("pbig256x256", DP_TILE_PBIG_256x256))
+         ("pbig320x256", DP_TILE_PBIG_320x256), ("pbig256x256", DP_TILE_PBIG_256x256),
+         ("dual256x128", DP_TILE_DUAL_256x128))
 N256 = (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
         DP_TILE_DEEP5_256x256, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256, DP_TILE_PBIG_320x256,
         DP_TILE_PBIG_256x256)
@@ -27,6 +28,8 @@ SHAPES = [  # (name, M, N, K, kw)
     ("qkv", 20195, 3072, 1024, {}),
     ("proj+res", 20195, 1024, 1024, {"acc": True}),
     ("fc1+gelu", 20195, 4096, 1024, {"gelu": True}),
+    ("fc1 nogelu", 20195, 4096, 1024, {}),
+    ("sq4096", 4096, 4096, 4096, {}),
     ("fc2+res", 20195, 1024, 4096, {"acc": True}),
     ("conv3x3 768^2 256->256", 768 * 768, 256, 2304, {"conv": 768}),
     ("conv3x3 384^2 256->256", 384 * 384, 256, 2304, {"conv": 384}),
@@ -98,10 +101,14 @@ def main():
                                  ldc=dc[2] if dc else None)  # noqa: E731
             ms = timeit(f, args.iters)
             res.append(f"{tname} {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
-            if args.ablate and tname.startswith("big"):
+            if args.ablate and (tname.startswith("big") or tname.startswith("8ph") or tname.startswith("p8")
+                                or tname.startswith("dual")):
                 from depth_pro import _lib
                 parts = []
-                for flags, lab in ((1, "nostore"), (2, "noload"), (3, "nostore+noload"), (4, "nomfma"), (5, "nomfma+nostore")):
+                abl = ((1, "nostore"), (2, "noload"), (3, "nostore+noload"), (4, "nomfma"), (5, "nomfma+nostore"))
+                if not tname.startswith("big"):
+                    abl = abl[:1]
+                for flags, lab in abl:
                     _lib.load().dp_gemm_debug_flags(flags)
                     parts.append(f"{lab} {timeit(f, args.iters)*1e3:.1f}")
                 _lib.load().dp_gemm_debug_flags(args.dbg)
