@@ -262,6 +262,17 @@ int dp_infer_epilogue(const float* canonical, int32_t src_h, int32_t src_w, cons
                       float* f_px_out, int32_t* nonfinite, dp_stream_t stream);
 
 /*
+ * dp_resize_u8_cv: cv2.resize of an 8-bit HWC 3-channel frame to OH x OW -- the reference's
+ * --downscale_factor (generate_depth_maps.py:95-110: INTER_AREA for factor < 1, INTER_LINEAR
+ * otherwise, new size int(H * factor) x int(W * factor)).  OpenCV 4.x's published fixed-point
+ * bilinear (11-bit coefficients) and area-averaging rules, restated in oracle/cv_resize_oracle.py
+ * (parity unpinned vs a cv2 binary: none is available).
+ */
+enum { DP_CV_INTER_LINEAR = 1, DP_CV_INTER_AREA = 3 };   /* cv2's constants */
+int dp_resize_u8_cv(const uint8_t* src, int32_t H, int32_t W, uint8_t* dst, int32_t OH, int32_t OW,
+                    int32_t interpolation, dp_stream_t stream);
+
+/*
  * dp_depth_to_points: camera-space point cloud of a depth map -- the reference's
  * depth_to_3d (img_to_normalized_pointcloud.py:819-856), used before its PLY write-out
  * (:1318).  valid = !isnan(depth) && depth > 0, points in row-major pixel order (numpy

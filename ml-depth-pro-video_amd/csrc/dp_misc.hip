@@ -331,6 +331,101 @@ __global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW
   }
 }
 
+// ------------------------------------------------- cv2.resize for 8-bit RGB frames
+// The reference's --downscale_factor (generate_depth_maps.py:95-110): cv2.resize, INTER_AREA for
+// factor < 1 and INTER_LINEAR otherwise, on the uint8 HWC frame.  OpenCV 4.x's published
+// algorithms (imgproc resize.cpp; restated in oracle/cv_resize_oracle.py): fixed-point bilinear
+// with 11-bit coefficients (SIMD vertical form, scalar form in the row tail), and area
+// averaging (integer-scale cells; fractional cell weights otherwise, float sums in table order,
+// no FMA contraction so that every rounding is OpenCV's).  One thread per output pixel.
+__device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v); }
+__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+__device__ __forceinline__ void cv_lin_tap(int d, double scale, int n, bool clamp_index, int& i0, int& w0, int& w1) {
+  float f = (float)((d + 0.5) * scale - 0.5);
+  int sidx = (int)floorf(f);
+  f = __fsub_rn(f, (float)sidx);
+  if (clamp_index) {
+    if (sidx < 0) { f = 0.f; sidx = 0; }
+    if (sidx >= n - 1) { f = 0.f; sidx = n - 1; }
+  }
+  i0 = sidx;
+  w0 = cv_round(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
+  w1 = cv_round(__fmul_rn(f, 2048.f));
+}
+
+// one axis of computeResizeAreaTab for output index d: visits (source index, alpha) in table order
+template <typename F>
+__device__ __forceinline__ void cv_area_taps(int d, double scale, int ssize, F&& f) {
+  const double fs1 = d * scale, fs2 = fs1 + scale;
+  const double cell = fmin(scale, ssize - fs1);
+  int s1 = (int)ceil(fs1), s2 = (int)floor(fs2);
+  s2 = min(s2, ssize - 1);
+  s1 = min(s1, s2);
+  if (s1 - fs1 > 1e-3) f(s1 - 1, (float)((s1 - fs1) / cell));
+  for (int sx = s1; sx < s2; ++sx) f(sx, (float)(1.0 / cell));
+  if (fs2 - s2 > 1e-3) f(s2, (float)(fmin(fmin(fs2 - s2, 1.0), cell) / cell));
+}
+
+// mode 0: INTER_LINEAR; 1: INTER_AREA integer cells; 2: INTER_AREA fractional cells
+__global__ void __launch_bounds__(256) cv_resize_kernel(const uint8_t* __restrict__ src, int H, int W,
+                                                        uint8_t* __restrict__ dst, int OH, int OW, int mode,
+                                                        double scale_y, double scale_x, int isy, int isx,
+                                                        int tail0) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)OH * OW) return;
+  const int dy = (int)(i / OW), dx = (int)(i - (long long)dy * OW);
+  uint8_t* o = dst + i * 3;
+  if (mode == 0) {
+    int x0, ax0, ax1, y0, by0, by1;
+    cv_lin_tap(dx, scale_x, W, true, x0, ax0, ax1);
+    cv_lin_tap(dy, scale_y, H, false, y0, by0, by1);
+    const int x1 = min(x0 + 1, W - 1);
+    const int r0 = min(max(y0, 0), H - 1), r1 = min(max(y0 + 1, 0), H - 1);
+    const uint8_t* s0 = src + (long long)r0 * W * 3;
+    const uint8_t* s1 = src + (long long)r1 * W * 3;
+    #pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int h0 = s0[x0 * 3 + c] * ax0 + s0[x1 * 3 + c] * ax1;
+      const int h1 = s1[x0 * 3 + c] * ax0 + s1[x1 * 3 + c] * ax1;
+      int v;
+      if (dx * 3 + c >= tail0) v = (h0 * by0 + h1 * by1 + (1 << 21)) >> 22;          // scalar row tail
+      else v = ((((h0 >> 4) * by0) >> 16) + (((h1 >> 4) * by1) >> 16) + 2) >> 2;   // SIMD form
+      o[c] = sat_u8(v);
+    }
+  } else if (mode == 1) {
+    int sum[3] = {0, 0, 0};
+    for (int a = 0; a < isy; ++a) {
+      const uint8_t* r = src + ((long long)(dy * isy + a) * W + (long long)dx * isx) * 3;
+      for (int b = 0; b < isx; ++b) {
+        sum[0] += r[3 * b]; sum[1] += r[3 * b + 1]; sum[2] += r[3 * b + 2];
+      }
+    }
+    const float sc = 1.f / (float)(isx * isy);
+    #pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      int v;
+      if (isx == 2 && isy == 2 && dx < tail0) v = (sum[c] + 2) >> 2;     // SIMD form of the 2 x 2 cells
+      else v = cv_round(__fmul_rn((float)sum[c], sc));
+      o[c] = sat_u8(v);
+    }
+  } else {
+    float acc[3] = {0.f, 0.f, 0.f};
+    cv_area_taps(dy, scale_y, H, [&](int sy, float beta) {
+      float buf[3] = {0.f, 0.f, 0.f};
+      const uint8_t* r = src + (long long)sy * W * 3;
+      cv_area_taps(dx, scale_x, W, [&](int sx, float alpha) {
+        #pragma unroll
+        for (int c = 0; c < 3; ++c) buf[c] = __fadd_rn(buf[c], __fmul_rn((float)r[sx * 3 + c], alpha));
+      });
+      #pragma unroll
+      for (int c = 0; c < 3; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(beta, buf[c]));
+    });
+    #pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = sat_u8(cv_round(acc[c]));
+  }
+}
+
 inline int blocks_for(long long n, int bs) { return (int)((n + bs - 1) / bs); }
 
 }  // namespace
@@ -448,6 +543,39 @@ extern "C" int dp_infer_epilogue(const float* canonical, int32_t SH, int32_t SW,
   hipLaunchKernelGGL(infer_epi_kernel, dim3(blocks_for((long long)H * W, 256)), dim3(256), 0, (hipStream_t)stream,
                      canonical, SH, SW, fov_deg, use_given, given_scale, (float)f_given, H, W, depth, f_px_out,
                      (int*)nonfinite);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dp_resize_u8_cv(const uint8_t* src, int32_t H, int32_t W, uint8_t* dst, int32_t OH, int32_t OW,
+                               int32_t interpolation, dp_stream_t stream) {
+  if (!src || !dst) return DP_ERR_ARG;
+  if (H <= 0 || W <= 0 || OH <= 0 || OW <= 0) return DP_ERR_SHAPE;
+  if (interpolation != DP_CV_INTER_LINEAR && interpolation != DP_CV_INTER_AREA) return DP_ERR_ARG;
+  // cv::resize: inv_scale = dsize / ssize, scale = 1 / inv_scale (doubles)
+  const double sx = 1.0 / ((double)OW / W), sy = 1.0 / ((double)OH / H);
+  int mode = 0, isx = 0, isy = 0, tail0 = 0;
+  if (interpolation == DP_CV_INTER_AREA && sx >= 1.0 && sy >= 1.0) {
+    isx = (int)lrint(sx);
+    isy = (int)lrint(sy);
+    const double eps = 2.220446049250313e-16;
+    if (fabs(sx - isx) < eps && fabs(sy - isy) < eps) {
+      mode = 1;
+      // the 2 x 2 SIMD loop takes whole groups of 16 pixels (48 bytes) of each row
+      tail0 = OW * 3 >= 48 ? (OW / 16) * 16 : 0;
+    } else {
+      mode = 2;
+    }
+  } else {
+    // (INTER_AREA on an upscale is INTER_LINEAR in OpenCV as well)
+    const int width = OW * 3;
+    int x = width >= 16 ? (width / 16) * 16 : 0;
+    while (x < width - 8) x += 8;
+    tail0 = x;     // first byte of each row that the scalar tail of the SIMD vertical pass writes
+  }
+  const long long n = (long long)OH * OW;
+  hipLaunchKernelGGL(cv_resize_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, (hipStream_t)stream, src, H, W, dst,
+                     OH, OW, mode, sy, sx, isy, isx, tail0);
   DP_CHECK_LAUNCH();
   return 0;
 }

@@ -17,6 +17,7 @@ DP_BF16, DP_F16, DP_F32 = 0, 1, 2
 DP_ACT_NONE, DP_ACT_RELU, DP_ACT_GELU = 0, 1, 2
 DP_A_DENSE, DP_A_CONV = 0, 1
 DP_STORE_ROWS, DP_STORE_DECONV2X2, DP_STORE_HEAD_PS = 0, 1, 2
+DP_CV_INTER_LINEAR, DP_CV_INTER_AREA = 1, 3
 (DP_TILE_AUTO, DP_TILE_128x128, DP_TILE_256x64, DP_TILE_256x32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x128,
  DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
@@ -34,7 +35,7 @@ EXPORTS = (
     "dp_abi_version", "dp_gemm", "dp_layernorm", "dp_attention", "dp_attention_log2q", "dp_normalize_u8",
     "dp_resize_bilinear", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
     "dp_merge_windows_range", "dp_fov_tail", "dp_infer_epilogue", "dp_gemm_workspace_size", "dp_gemm_plan",
-    "dp_depth_to_points", "dp_gemm_workspace_check",
+    "dp_depth_to_points", "dp_gemm_workspace_check", "dp_resize_u8_cv",
 )
 
 
@@ -106,6 +107,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "dp_infer_epilogue": [vp, i32, i32, vp, i32, f64, i32, i32, vp, vp, vp, vp],
         "dp_gemm_workspace_size": [],
         "dp_gemm_workspace_check": [vp, vp, vp],
+        "dp_resize_u8_cv": [vp, i32, i32, vp, i32, i32, i32, vp],
         "dp_depth_to_points": [vp, i32, i32, vp, f64, i32, vp, vp, vp, vp, vp],
         "dp_gemm_plan": [ctypes.POINTER(GemmArgs), ctypes.POINTER(i32), ctypes.POINTER(i32)],
     }

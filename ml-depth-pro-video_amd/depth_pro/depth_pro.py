@@ -107,13 +107,19 @@ class Transform:
         self.precision = precision
 
     def __call__(self, image) -> torch.Tensor:
-        a = np.asarray(image)
-        if a.ndim == 2:
-            a = a[:, :, None]
-        if a.dtype != np.uint8 or a.shape[2] != 3:
-            raise TypeError(f"transform expects an HxWx3 uint8 image, got {a.dtype} {a.shape}")
-        src = torch.from_numpy(np.ascontiguousarray(a)).to(self.device, non_blocking=True)
-        out = torch.empty(3, a.shape[0], a.shape[1], dtype=self.precision, device=self.device)
+        if torch.is_tensor(image):          # a uint8 HxWx3 frame already on the device (frame loops)
+            src = image.to(self.device)
+            if src.dtype != torch.uint8 or src.dim() != 3 or src.shape[2] != 3:
+                raise TypeError(f"transform expects an HxWx3 uint8 image, got {src.dtype} {tuple(src.shape)}")
+            src = src.contiguous()
+        else:
+            a = np.asarray(image)
+            if a.ndim == 2:
+                a = a[:, :, None]
+            if a.dtype != np.uint8 or a.shape[2] != 3:
+                raise TypeError(f"transform expects an HxWx3 uint8 image, got {a.dtype} {a.shape}")
+            src = torch.from_numpy(np.ascontiguousarray(a)).to(self.device, non_blocking=True)
+        out = torch.empty(3, src.shape[0], src.shape[1], dtype=self.precision, device=self.device)
         ops.normalize_u8(src, out)
         return out
 

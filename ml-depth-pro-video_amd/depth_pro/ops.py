@@ -313,3 +313,18 @@ def infer_epilogue(canonical: torch.Tensor, fov_deg: Optional[torch.Tensor], f_g
     check(_lib.load().dp_infer_epilogue(canonical.data_ptr(), SH, SW, _p(fov_deg), int(use_given),
                                         float(f_given) if use_given else 0.0, H, W, depth.data_ptr(),
                                         _p(f_px_out), _p(nonfinite), _stream(depth)), "dp_infer_epilogue")
+
+
+def resize_u8_cv(img: torch.Tensor, out_h: int, out_w: int, area: bool) -> torch.Tensor:
+    """cv2.resize of a uint8 HxWx3 device frame (dp_resize_u8_cv): INTER_AREA if `area`, else
+    INTER_LINEAR -- the reference's --downscale_factor picks INTER_AREA for factor < 1
+    (generate_depth_maps.py:95-110)."""
+    if img.dtype != torch.uint8 or img.dim() != 3 or img.shape[2] != 3:
+        raise _lib.DPError(f"resize_u8_cv expects a uint8 HxWx3 tensor, got {img.dtype} {tuple(img.shape)}")
+    img = img.contiguous()
+    H, W = img.shape[0], img.shape[1]
+    out = torch.empty(out_h, out_w, 3, dtype=torch.uint8, device=img.device)
+    interp = _lib.DP_CV_INTER_AREA if area else _lib.DP_CV_INTER_LINEAR
+    check(_lib.load().dp_resize_u8_cv(img.data_ptr(), H, W, out.data_ptr(), out_h, out_w, interp, _stream(out)),
+          "dp_resize_u8_cv")
+    return out

@@ -71,16 +71,6 @@ def _write_png(path: str, arr: np.ndarray) -> None:
         Image.fromarray(np.ascontiguousarray(arr)).save(path, compress_level=1)
 
 
-def _resize_u8(image: np.ndarray, factor: float) -> np.ndarray:
-    """Host stand-in for cv2.resize(INTER_AREA if factor < 1 else INTER_LINEAR) (reference :95-110)."""
-    from PIL import Image
-
-    h, w = image.shape[:2]
-    nh, nw = int(h * factor), int(w * factor)
-    resample = Image.BOX if factor < 1.0 else Image.BILINEAR
-    return np.asarray(Image.fromarray(image).resize((nw, nh), resample=resample))
-
-
 _MODEL = {}
 
 
@@ -126,12 +116,25 @@ def _device() -> torch.device:
 
 
 def _load(image_path: str, downscale_factor: float):
+    """Decode (host thread): the frame and its EXIF focal length, scaled by --downscale_factor as
+    the reference does (:108-110); the resize itself runs on the GPU (`_downscale`)."""
     image, _, f_px = depth_pro.load_rgb(image_path)
-    if downscale_factor != 1.0 and downscale_factor > 0:
-        image = _resize_u8(image, downscale_factor)
-        if f_px is not None:
-            f_px = f_px * downscale_factor
+    if downscale_factor != 1.0 and downscale_factor > 0 and f_px is not None:
+        f_px = f_px * downscale_factor
     return image, f_px
+
+
+def _downscale(image: np.ndarray, downscale_factor: float, device: torch.device):
+    """The reference's cv2.resize (:95-107: new size int(H * f) x int(W * f), INTER_AREA for f < 1,
+    INTER_LINEAR otherwise) on the GPU (dp_resize_u8_cv): uint8 upload, uint8 frame on the device.
+    Without a factor the host frame is returned as is (the transform uploads it)."""
+    if downscale_factor == 1.0 or downscale_factor <= 0:
+        return image
+    from depth_pro import ops
+
+    h, w = image.shape[:2]
+    src = torch.from_numpy(np.ascontiguousarray(image)).to(device, non_blocking=True)
+    return ops.resize_u8_cv(src, int(h * downscale_factor), int(w * downscale_factor), area=downscale_factor < 1.0)
 
 
 def _encode(depth_np: np.ndarray, output_path: str, colored: bool, cmap: str) -> str:
@@ -151,8 +154,10 @@ def generate_depth_map(image_path, output_path=None, downscale_factor=1.0, half_
             output_path = f"{base_name}_depth.png"
         model, transform = _model(_device(), half_precision)
         image, f_px = _load(image_path, downscale_factor)
+        image = _downscale(image, downscale_factor, _device())
         with torch.no_grad():
             depth = model.infer(transform(image), f_px=f_px)["depth"]
+        model.last_status().check()
         return _encode(depth.detach().cpu().numpy(), output_path, colored, cmap)
     except Exception as e:  # reference :147-151: report and skip the frame
         print(f"Error generating depth map for {image_path}: {str(e)}")
@@ -236,6 +241,8 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 if nxt < len(mine):
                     futs[mine[nxt]] = dec.submit(_load, image_paths[mine[nxt]], downscale_factor)
                     nxt += 1
+                if downscale_factor != 1.0 and downscale_factor > 0:
+                    image = _downscale(image, downscale_factor, getattr(transform, "device", None) or _device())
                 with torch.no_grad():
                     pred = model.infer(transform(image), f_px=f_px)
                     depth = pred["depth"]
@@ -277,12 +284,13 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
     return successful
 
 
-def _points(depth: torch.Tensor, f_px, image: np.ndarray):
+def _points(depth: torch.Tensor, f_px, image):
     """Queue the frame's point cloud on the GPU (depth_to_3d, img_to_normalized_pointcloud.py:819-856)
     and its copy into pinned host buffers, on the current stream, without a host synchronisation:
     full-size buffers + the point count (the writer slices them after the frame's event)."""
     h, w = depth.shape
-    rgb = torch.from_numpy(np.ascontiguousarray(image)).to(depth.device, non_blocking=True)
+    rgb = image.to(depth.device) if torch.is_tensor(image) else \
+        torch.from_numpy(np.ascontiguousarray(image)).to(depth.device, non_blocking=True)
     xyz, _, cols, count = PC.depth_to_points_async(depth, f_px, w, h, rgb=rgb)
     out = []
     for t in (xyz, cols, count):

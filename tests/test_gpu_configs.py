@@ -177,3 +177,29 @@ def test_frame_loop_drops_exactly_the_failed_frame(tmp_path, cuda):
     assert n == 2
     assert sorted(os.listdir(out)) == ["output_0000_depth.png", "output_0000_points.ply",
                                        "output_0002_depth.png", "output_0002_points.ply"]
+
+
+@pytest.mark.parametrize("factor", [0.5, 0.6, 1.5])
+def test_frame_loop_downscale_factor(tmp_path, cuda, factor):
+    """--downscale_factor (reference generate_depth_maps.py:95-110): the loop resizes on the GPU
+    (dp_resize_u8_cv) exactly as the cv2.resize restatement does (oracle/cv_resize_oracle.py:
+    INTER_AREA below 1, INTER_LINEAR above; parity vs a cv2 binary unpinned), and the written PNG
+    is the colour map of the model's depth for that resized frame."""
+    from PIL import Image
+
+    import generate_depth_maps as G
+    from oracle import cv_resize_oracle as CV
+
+    src = tmp_path / "frames"
+    src.mkdir()
+    img = frame(40, 250, 330)
+    Image.fromarray(img).save(src / "output_0000.png")
+    out = tmp_path / "out"
+    assert G.batch_generate_depth_maps(str(src), str(out), pattern="output_*.png", downscale_factor=factor) == 1
+    small = CV.cv2_resize_u8(img, factor)
+    model, transform = G._model(cuda, False)
+    with torch.no_grad():
+        depth = model.infer(transform(small))["depth"].cpu().numpy()
+    png = np.asarray(Image.open(out / "output_0000_depth.png"))
+    assert png.shape == small.shape
+    assert np.array_equal(png, G.colorize_depth(depth))
