@@ -70,3 +70,25 @@ def synthetic_state_dict(seed: int = 0, use_fov_head: bool = True) -> Dict[str, 
     for key, shape in param_spec(use_fov_head).items():
         sd[key] = synthetic_tensor(key, shape, seed)
     return sd
+
+
+# Stress set (parity margin outside the benign synthetic distribution): real
+# DINOv2 checkpoints carry LayerScale gammas well above 0.1 and a few residual-stream channels
+# with very large activations.  Same tensors as `synthetic_state_dict`, except every LayerScale
+# gamma x STRESS_LS, and in every ViT block the fc2 bias of STRESS_CHANNELS raised by
+# STRESS_BIAS (the outliers then grow block by block through the residual stream).
+STRESS_LS = 5.0
+STRESS_CHANNELS = (7, 300, 901)
+STRESS_BIAS = 20.0
+
+
+def stressed_state_dict(seed: int = 0, use_fov_head: bool = True) -> Dict[str, torch.Tensor]:
+    sd = synthetic_state_dict(seed, use_fov_head)
+    for k, v in sd.items():
+        if k.endswith(".gamma"):
+            sd[k] = v * STRESS_LS
+        elif k.endswith("mlp.fc2.bias"):
+            v = v.clone()
+            v[list(STRESS_CHANNELS)] += STRESS_BIAS
+            sd[k] = v
+    return sd

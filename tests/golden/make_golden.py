@@ -6,6 +6,7 @@ not exist on the GPU box):
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py            # all fixtures
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --stages   # golden_stages_frame0.npz only
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --io       # load_rgb + 4K infer fixtures
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --stress   # golden_stress_frame0.npz (stressed weights)
 
 What it does
 ------------
@@ -395,6 +396,43 @@ def io_fixtures(ref, model, transform, t0):
     print(f"[golden] infer 4K done ({time.time()-t0:.1f}s): f_px={float(p['focallength_px']):.3f}")
 
 
+def stress_fixture(model, transform, t0):
+    """golden_stress_frame0.npz: the reference forward on frame 0 with the STRESSED synthetic
+    weights (depth_pro.weights.stressed_state_dict: LayerScale x5, outlier residual channels)."""
+    from depth_pro_amd_spec import stressed_state_dict  # noqa: see shim below
+
+    model.load_state_dict(stressed_state_dict(0), strict=True)
+    caps = {}
+    dec_fwd = model.decoder.forward
+
+    def dec_capture(e):
+        f, lo = dec_fwd(e)
+        caps["enc_absmax"] = np.array([float(t.abs().max()) for t in e])
+        caps["features_absmax"], caps["lowres_absmax"] = float(f.abs().max()), float(lo.abs().max())
+        return f, lo
+
+    model.decoder.forward = dec_capture
+    hooks, peaks = [], {}
+    for name in ("patch_encoder", "image_encoder"):
+        vit = getattr(model.encoder, name)
+        hooks.append(vit.blocks[23].register_forward_hook(
+            lambda m, i, o, name=name: peaks.__setitem__(name, float(o.abs().max()))))
+    x = transform(frame(0)).unsqueeze(0)
+    with torch.no_grad():
+        canonical, fov_deg = model.forward(x)
+    for h in hooks:
+        h.remove()
+    model.decoder.forward = dec_fwd
+    print(f"[golden] stress forward done ({time.time()-t0:.1f}s): fov={fov_deg.item():.4f} residual peaks {peaks} "
+          f"encodings |max| {caps['enc_absmax']} features |max| {caps['features_absmax']:.1f}")
+    np.savez_compressed(
+        os.path.join(HERE, "golden_stress_frame0.npz"), frame_seed=0, fov_deg=fov_deg.numpy().reshape(-1),
+        canonical_sub8=sub(canonical[0, 0], 8), canonical_stats=stats(canonical),
+        residual_absmax=np.array([peaks["patch_encoder"], peaks["image_encoder"]]),
+        enc_absmax=caps["enc_absmax"], features_absmax=np.array(caps["features_absmax"]),
+        lowres_absmax=np.array(caps["lowres_absmax"]))
+
+
 def main():
     t0 = time.time()
     torch.set_num_threads(len(os.sched_getaffinity(0)))
@@ -425,6 +463,8 @@ def main():
         assert tuple(ref_sd[k].shape) == tuple(shp), (k, ref_sd[k].shape, shp)
     print(f"[golden] reference model built: {len(ref_sd)} keys, "
           f"{sum(v.numel() for v in ref_sd.values())} params ({time.time()-t0:.1f}s)")
+    if "--stress" in sys.argv:
+        return stress_fixture(model, transform, t0)
     sd = synthetic_state_dict(0)
     model.load_state_dict(sd, strict=True)
     print(f"[golden] synthetic weights loaded ({time.time()-t0:.1f}s)")
@@ -585,5 +625,6 @@ if __name__ == "__main__":
     shim = types.ModuleType("depth_pro_amd_spec")
     shim.param_spec = importlib.import_module("_dpamd.spec").param_spec
     shim.synthetic_state_dict = importlib.import_module("_dpamd.weights").synthetic_state_dict
+    shim.stressed_state_dict = importlib.import_module("_dpamd.weights").stressed_state_dict
     sys.modules["depth_pro_amd_spec"] = shim
     main()

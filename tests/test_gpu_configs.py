@@ -203,3 +203,37 @@ def test_frame_loop_downscale_factor(tmp_path, cuda, factor):
     png = np.asarray(Image.open(out / "output_0000_depth.png"))
     assert png.shape == small.shape
     assert np.array_equal(png, G.colorize_depth(depth))
+
+
+def test_stressed_weights_mixed_precision_margin(cuda, golden_dir):
+    """Parity outside the benign synthetic distribution (LayerScale x5 and outlier residual
+    channels, depth_pro.weights.stressed_state_dict; reference forward: golden_stress_frame0.npz)
+    in the default mixed mode (bf16 ViTs, f16 decoder): every output finite (no f16 overflow in
+    the decoder; the frame's FrameStatus is healthy) and the measured error printed and bounded.
+    Bound: 1e-3 on depth like the benign set -- if this fails, the f16 decoder is where the margin
+    ends."""
+    import depth_pro
+    from depth_pro.depth_pro import DepthPro, Transform, _compute_dtype
+    from depth_pro.weights import stressed_state_dict
+
+    g = np.load(f"{golden_dir}/golden_stress_frame0.npz")
+    m = DepthPro(use_fov_head=True, compute_dtype=_compute_dtype(torch.float32))
+    m.load_state_dict(stressed_state_dict(0), strict=True)
+    m = m.to(cuda).eval()
+    t = Transform(cuda, torch.float32)
+    with torch.no_grad():
+        pred = m.infer(t(frame(0)))
+        canonical, fov = m.forward(t(frame(0)).unsqueeze(0))
+    m.last_status().check()
+    depth = pred["depth"].cpu().numpy()
+    assert np.isfinite(depth).all() and np.isfinite(float(pred["focallength_px"]))
+    c = canonical[0, 0, ::8, ::8].float().cpu().numpy()
+    e_c = rel_l1(c, g["canonical_sub8"])
+    W = 1536.0
+    f_ref = 0.5 * W / np.tan(0.5 * np.deg2rad(float(g["fov_deg"][0])))
+    d_ref = 1.0 / np.clip(g["canonical_sub8"].astype(np.float64) * (W / f_ref), 1e-4, 1e4)
+    e_d = rel_l1(depth[::8, ::8], d_ref)
+    e_f = abs(fov.item() - float(g["fov_deg"][0])) / abs(float(g["fov_deg"][0]))
+    print(f"\nstressed weights (mixed): canonical rel-L1 {e_c:.3e}  depth rel-L1 {e_d:.3e}  fov rel {e_f:.2e}; "
+          f"reference residual |max| {g['residual_absmax']}, decoder features |max| {float(g['features_absmax']):.1f}")
+    assert e_d < 1e-3 and e_f < 1e-3
