@@ -494,6 +494,28 @@ __device__ __forceinline__ void epilogue_rows_buf(const GemmP& p, const ColConst
   }
 }
 
+// Epilogue variants.  ROWLD: the launch reads per-row operands (R1 / R2, pos, the fp32 C it
+// accumulates into) or stores through a remap (deconv pixel shuffle, row groups, the fused /
+// composed heads).  Without any of those the epilogue issues no loads at all, and the compiler
+// then needs no `s_waitcnt vmcnt(0)` between row batches: with a (runtime-conditional) load in a
+// batch it must wait for every older VMEM op, i.e. for the previous batches' stores, which
+// serialised the epilogue on store latency (fc1: 50 us of 225).
+__host__ __device__ inline bool needs_rowld(const GemmP& p) {
+  return p.R1 || p.R2 || p.pos || p.accumulate || p.store_mode != DP_STORE_ROWS || p.row_group || p.head_corr ||
+         p.head_w;
+}
+template <bool ROWLD>
+__device__ __forceinline__ GemmP epi_params(const GemmP& p) {
+  if constexpr (ROWLD) {
+    return p;
+  } else {
+    GemmP q = p;
+    q.R1 = nullptr; q.R2 = nullptr; q.pos = nullptr; q.accumulate = 0;
+    q.store_mode = DP_STORE_ROWS; q.row_group = 0; q.head_corr = nullptr; q.head_w = nullptr;
+    return q;
+  }
+}
+
 // DP_STORE_HEAD_PS epilogue (depth head tail, depth_pro.py:182-207, composed at
 // pack time): the GEMM ran the 3x3 conv of head.2 over the 2x-upsampled map as a
 // 3x3 conv of the pre-upsampling map h0 whose N = 128 columns are (parity q =
@@ -653,7 +675,7 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
 
 // NW = waves per workgroup: 8 (one workgroup per CU), or 4 (two workgroups per CU, each
 // wave one per SIMD: one workgroup's epilogue runs beside the other's K loop).
-template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, int NW = 8>
+template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, int NW = 8, bool ROWLD = true>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(const GemmP p) {
   // 8 waves as WM x WN; the 512 x 128 tile (N = 128 layers) uses 4 x 2 so that every
   // wave still owns a 128 x 64 sub-tile (same fragment reuse as the 256 x 256 tile);
@@ -937,13 +959,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
         for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
         ms[it] = m0 + wm * TM + q * 32 + row;
       }
-      if constexpr (TN % 32 == 0) {
+      if constexpr (TN % 32 == 0 && ROWLD) {
         if (p.store_mode == DP_STORE_HEAD_PS) {
           head_ps_rows<NITC>(p, cc, ms, n_l, v, lane);
           continue;
         }
       }
-      epilogue_rows<K_, NITC, CONV && BM == 512 && !RELU>(p, cc, ms, n_l, v);
+      epilogue_rows<K_, NITC, CONV && BM == 512 && !RELU && ROWLD>(epi_params<ROWLD>(p), cc, ms, n_l, v);
     }
   }
   DP_STAMP(st3_);
@@ -1162,7 +1184,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
 // tiles remain).  Quadrant order (qm,qn): (0,0) (0,1) (1,0) (1,1); reads:
 // p0 A(qm0)+B(qn0), p1 B(qn1), p2 A(qm1), p3 none.  Issue order of tile
 // t+1 / t+2 halves: p0 A0(t+1), p1 A1(t+1), p2 B0(t+2), p3 B1(t+2).
-template <typename K_, bool CONV, bool RELU>
+template <typename K_, bool CONV, bool RELU, bool ROWLD = true>
 __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
   constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
   constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
@@ -1340,7 +1362,7 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
         for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
         ms[it] = m0 + wm * TM + q * 32 + row;
       }
-      epilogue_rows<K_, 2>(p, cc, ms, n_l, v);
+      epilogue_rows<K_, 2>(epi_params<ROWLD>(p), cc, ms, n_l, v);
     }
   }
 }
@@ -1351,10 +1373,15 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
   p.tiles_n = (p.N + 255) / 256;
   p.tiles_m = (p.M + 255) / 256;
   dim3 grid(p.tiles_n * p.tiles_m);
-  if (conv && p.relu_a) hipLaunchKernelGGL((gemm_8ph_kernel<K_, true, true>), grid, dim3(512), 0, s, p);
-  else if (conv) hipLaunchKernelGGL((gemm_8ph_kernel<K_, true, false>), grid, dim3(512), 0, s, p);
-  else if (p.relu_a) hipLaunchKernelGGL((gemm_8ph_kernel<K_, false, true>), grid, dim3(512), 0, s, p);
-  else hipLaunchKernelGGL((gemm_8ph_kernel<K_, false, false>), grid, dim3(512), 0, s, p);
+  const bool rl = needs_rowld(p) || (p.dbg & (1 << 20));   // debug 1 << 20: the general epilogue (A/B)
+#define DP_8PH(C_, R_) do { \
+    if (rl) hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, true>), grid, dim3(512), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, false>), grid, dim3(512), 0, s, p); } while (0)
+  if (conv && p.relu_a) DP_8PH(true, true);
+  else if (conv) DP_8PH(true, false);
+  else if (p.relu_a) DP_8PH(false, true);
+  else DP_8PH(false, false);
+#undef DP_8PH
   DP_CHECK_LAUNCH();
   return 0;
 }
@@ -1811,14 +1838,18 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   p.tiles_n = (p.N + BN - 1) / BN;
   p.tiles_m = (p.M + BM - 1) / BM;
   dim3 grid(p.tiles_n * p.tiles_m);
-  if (conv && p.relu_a)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, true, true>), grid, dim3(NT_BIG), 0, s, p);
-  else if (conv)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, true, false>), grid, dim3(NT_BIG), 0, s, p);
-  else if (p.relu_a)
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, true>), grid, dim3(NT_BIG), 0, s, p);
-  else
-    hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, false, false>), grid, dim3(NT_BIG), 0, s, p);
+  // the load-free epilogue for launches without per-row operands (needs_rowld), on the BK = 64
+  // engines the planner picks; debug 1 << 20: always the general one (A/B)
+  const bool rl = needs_rowld(p) || (p.dbg & (1 << 20)) || BKT != 64;
+#define DP_BIG(C_, R_) do { \
+    if (rl) hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, C_, R_, 8, true>), grid, dim3(NT_BIG), 0, s, p); \
+    else if constexpr (BKT == 64) hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, C_, R_, 8, false>), grid, dim3(NT_BIG), 0, s, p); \
+  } while (0)
+  if (conv && p.relu_a) DP_BIG(true, true);
+  else if (conv) DP_BIG(true, false);
+  else if (p.relu_a) DP_BIG(false, true);
+  else DP_BIG(false, false);
+#undef DP_BIG
   DP_CHECK_LAUNCH();
   return 0;
 }

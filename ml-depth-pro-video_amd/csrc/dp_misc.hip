@@ -342,6 +342,7 @@ __device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v
 __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
 
 __device__ __forceinline__ void cv_lin_tap(int d, double scale, int n, bool clamp_index, int& i0, int& w0, int& w1) {
+#pragma clang fp contract(off)
   float f = (float)((d + 0.5) * scale - 0.5);
   int sidx = (int)floorf(f);
   f = __fsub_rn(f, (float)sidx);
@@ -357,6 +358,7 @@ __device__ __forceinline__ void cv_lin_tap(int d, double scale, int n, bool clam
 // one axis of computeResizeAreaTab for output index d: visits (source index, alpha) in table order
 template <typename F>
 __device__ __forceinline__ void cv_area_taps(int d, double scale, int ssize, F&& f) {
+#pragma clang fp contract(off)
   const double fs1 = d * scale, fs2 = fs1 + scale;
   const double cell = fmin(scale, ssize - fs1);
   int s1 = (int)ceil(fs1), s2 = (int)floor(fs2);
@@ -372,6 +374,7 @@ __global__ void __launch_bounds__(256) cv_resize_kernel(const uint8_t* __restric
                                                         uint8_t* __restrict__ dst, int OH, int OW, int mode,
                                                         double scale_y, double scale_x, int isy, int isx,
                                                         int tail0) {
+#pragma clang fp contract(off)   // every product and sum rounded on its own, as OpenCV's SSE code does
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)OH * OW) return;
   const int dy = (int)(i / OW), dx = (int)(i - (long long)dy * OW);
