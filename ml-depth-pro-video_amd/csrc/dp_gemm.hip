@@ -494,26 +494,77 @@ __device__ __forceinline__ void epilogue_rows_buf(const GemmP& p, const ColConst
   }
 }
 
-// Epilogue variants.  ROWLD: the launch reads per-row operands (R1 / R2, pos, the fp32 C it
-// accumulates into) or stores through a remap (deconv pixel shuffle, row groups, the fused /
-// composed heads).  Without any of those the epilogue issues no loads at all, and the compiler
-// then needs no `s_waitcnt vmcnt(0)` between row batches: with a (runtime-conditional) load in a
-// batch it must wait for every older VMEM op, i.e. for the previous batches' stores, which
-// serialised the epilogue on store latency (fc1: 50 us of 225).
+// Epilogue variants.  needs_rowld: the launch reads per-row operands (R1 / R2, pos, the fp32 C
+// it accumulates into) or stores through a remap (deconv pixel shuffle, row groups, the fused /
+// composed heads).  Without any of those (and with a 16-bit C) the engines take the load-free
+// epilogue_mfma below: no loads at all, so the compiler needs no `s_waitcnt vmcnt(0)` between
+// row batches (in the general epilogue a runtime-conditional load in a batch makes it wait for
+// every older VMEM op, i.e. for the previous batches' stores: the epilogue serialised on store
+// latency, fc1 221.6 -> 211.2 us and qkv 146.3 -> 135.1 us without it).
 __host__ __device__ inline bool needs_rowld(const GemmP& p) {
   return p.R1 || p.R2 || p.pos || p.accumulate || p.store_mode != DP_STORE_ROWS || p.row_group || p.head_corr ||
          p.head_w;
 }
-template <bool ROWLD>
-__device__ __forceinline__ GemmP epi_params(const GemmP& p) {
-  if constexpr (ROWLD) {
-    return p;
-  } else {
-    GemmP q = p;
-    q.R1 = nullptr; q.R2 = nullptr; q.pos = nullptr; q.accumulate = 0;
-    q.store_mode = DP_STORE_ROWS; q.row_group = 0; q.head_corr = nullptr; q.head_w = nullptr;
-    return q;
+// Load-free epilogue in the MFMA register layout (no per-row operands, 16-bit C): lane
+// (t = lane & 15, g = lane >> 4) of accumulator fragment (fm, fn) holds token row fm * 16 + t,
+// channels fn * 16 + 4 g .. + 3.  bias / ACT / gamma are applied right there, on all FM x FN x 4
+// values of the lane at once (no per-row batches: the compiler interleaves 128 independent GELU
+// chains), packed to 16 bits and staged through the wave's LDS slab as [rows][TN] 16-bit rows
+// (16-B chunks XOR-swizzled by row), which are read back row-major and stored as whole row
+// segments (TN * 2 bytes per row, 16 B per lane).  PF fragment rows per pass (slab: PF * 16 *
+// TN * 2 bytes per wave).  LDS operations of one wave complete in order, so the write -> read
+// -> next pass's write sequence needs no barrier (the slab is the wave's own).
+template <typename K_, int ACT, int FM, int FN, int TN, int PF>
+__device__ __forceinline__ void epilogue_mfma(const GemmP& p, f32x4_t (&acc)[FM][FN], char* slab, int lane,
+                                              int m_base, int n_base) {
+  constexpr int CH = TN / 8;            // 16-B chunks per staged row
+  constexpr int RPI = 64 / CH;          // rows per read-back instruction
+  static_assert(FM % PF == 0 && (CH == 8 || CH == 4), "tile");
+  const int t = lane & 15, g = lane >> 4;
+  float bias[FN][4], gam[FN][4];
+  #pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int n = n_base + fn * 16 + 4 * g;
+    const bool ok = n < p.N;
+    const float4 b = (p.bias && ok) ? *(const float4*)(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 q = (p.gamma && ok) ? *(const float4*)(p.gamma + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+    bias[fn][0] = b.x; bias[fn][1] = b.y; bias[fn][2] = b.z; bias[fn][3] = b.w;
+    gam[fn][0] = q.x; gam[fn][1] = q.y; gam[fn][2] = q.z; gam[fn][3] = q.w;
   }
+  #pragma unroll
+  for (int f0 = 0; f0 < FM; f0 += PF) {
+    #pragma unroll
+    for (int fm = 0; fm < PF; ++fm)
+      #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        float x[4];
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[f0 + fm][fn][r] + bias[fn][r];
+          if constexpr (ACT == DP_ACT_RELU) v = fmaxf(v, 0.f);
+          else if constexpr (ACT == DP_ACT_GELU) v = gelu_erf(v);
+          x[r] = v * gam[fn][r];
+        }
+        const int row = fm * 16 + t;
+        const int chunk = fn * 2 + (g >> 1);
+        uint2 w;
+        w.x = K_::pack2(x[0], x[1]);
+        w.y = K_::pack2(x[2], x[3]);
+        *(uint2*)(slab + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4) + (g & 1) * 8) = w;
+      }
+    #pragma unroll
+    for (int k = 0; k < PF * 16 / RPI; ++k) {
+      const int row = k * RPI + lane / CH, chunk = lane % CH;
+      const uint4 d = *(const uint4*)(slab + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4));
+      const int m = m_base + f0 * 16 + row, n = n_base + chunk * 8;
+      if (m < p.M && n < p.N) *(uint4*)((u16*)p.C + (long long)m * p.ldc + n) = d;
+    }
+  }
+}
+// EACT of the load-free engine variants: the compile-time epilogue (-1: the general, runtime one)
+__host__ inline int fast_epi_act(const GemmP& p) {
+  if (needs_rowld(p) || p.c_dtype == DP_F32 || (p.dbg & (1 << 20))) return -1;
+  return p.act;
 }
 
 // DP_STORE_HEAD_PS epilogue (depth head tail, depth_pro.py:182-207, composed at
@@ -675,7 +726,9 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
 
 // NW = waves per workgroup: 8 (one workgroup per CU), or 4 (two workgroups per CU, each
 // wave one per SIMD: one workgroup's epilogue runs beside the other's K loop).
-template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, int NW = 8, bool ROWLD = true>
+// EACT: -1 = the general epilogue (runtime operand set); DP_ACT_* = the load-free MFMA-layout
+// epilogue with that activation (epilogue_mfma; fast_epi_act decides on the host).
+template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, int NW = 8, int EACT = -1>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(const GemmP p) {
   // 8 waves as WM x WN; the 512 x 128 tile (N = 128 layers) uses 4 x 2 so that every
   // wave still owns a 128 x 64 sub-tile (same fragment reuse as the 256 x 256 tile);
@@ -921,6 +974,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
       for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j][0]), "v"(acc[i][j][1]), "v"(acc[i][j][2]), "v"(acc[i][j][3]));
     return;
   }
+  if constexpr (EACT >= 0) {
+    lds_barrier();  // the ring is free once every wave has left the K loop
+    constexpr int PF = (FM * 16 * TN * 2 * 8 <= SMEM) ? FM : FM / 2;
+    epilogue_mfma<K_, EACT, FM, FN, TN, PF>(p, acc, smem + wave * (PF * 16 * TN * 2), lane, m0 + wm * TM,
+                                            n0 + wn * TN);
+    return;
+  }
   // Epilogue through LDS: the MFMA layout gives each lane 4 columns of one row
   // (16 rows x 32-64 B per store instruction -- partial cache lines, measured at
   // ~half of the kernel's time on the ViT shapes).  Each wave instead parks 32
@@ -959,13 +1019,13 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
         for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
         ms[it] = m0 + wm * TM + q * 32 + row;
       }
-      if constexpr (TN % 32 == 0 && ROWLD) {
+      if constexpr (TN % 32 == 0) {
         if (p.store_mode == DP_STORE_HEAD_PS) {
           head_ps_rows<NITC>(p, cc, ms, n_l, v, lane);
           continue;
         }
       }
-      epilogue_rows<K_, NITC, CONV && BM == 512 && !RELU && ROWLD>(epi_params<ROWLD>(p), cc, ms, n_l, v);
+      epilogue_rows<K_, NITC, CONV && BM == 512 && !RELU>(p, cc, ms, n_l, v);
     }
   }
   DP_STAMP(st3_);
@@ -1184,7 +1244,7 @@ __global__ void __launch_bounds__(NT_BIG, 1) gemm_pbig_kernel(const GemmP p) {
 // tiles remain).  Quadrant order (qm,qn): (0,0) (0,1) (1,0) (1,1); reads:
 // p0 A(qm0)+B(qn0), p1 B(qn1), p2 A(qm1), p3 none.  Issue order of tile
 // t+1 / t+2 halves: p0 A0(t+1), p1 A1(t+1), p2 B0(t+2), p3 B1(t+2).
-template <typename K_, bool CONV, bool RELU, bool ROWLD = true>
+template <typename K_, bool CONV, bool RELU, int EACT = -1>
 __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
   constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
   constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
@@ -1335,6 +1395,11 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
     return;
   }
 
+  if constexpr (EACT >= 0) {
+    lds_barrier();   // the ring (128 KiB) is free: a 16 KiB slab per wave holds its whole 128 x 64 tile
+    epilogue_mfma<K_, EACT, 8, 4, 64, 8>(p, acc, smem + wave * 16384, lane, m0 + wm * TM, n0 + wn * TN);
+    return;
+  }
   // epilogue: identical to the big engine (LDS-staged, row-coalesced)
   lds_barrier();
   constexpr int SROW = TN + 4, CPR = TN / 8, RPI = 64 / CPR, NIT = 32 / RPI;
@@ -1362,7 +1427,7 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
         for (int r = 0; r < 4; ++r) { v[it][r] = lo[r]; v[it][4 + r] = hi[r]; }
         ms[it] = m0 + wm * TM + q * 32 + row;
       }
-      epilogue_rows<K_, 2>(epi_params<ROWLD>(p), cc, ms, n_l, v);
+      epilogue_rows<K_, 2>(p, cc, ms, n_l, v);
     }
   }
 }
@@ -1373,10 +1438,12 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
   p.tiles_n = (p.N + 255) / 256;
   p.tiles_m = (p.M + 255) / 256;
   dim3 grid(p.tiles_n * p.tiles_m);
-  const bool rl = needs_rowld(p) || (p.dbg & (1 << 20));   // debug 1 << 20: the general epilogue (A/B)
+  const int ea = fast_epi_act(p);   // debug 1 << 20: the general epilogue (A/B)
 #define DP_8PH(C_, R_) do { \
-    if (rl) hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, true>), grid, dim3(512), 0, s, p); \
-    else hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, false>), grid, dim3(512), 0, s, p); } while (0)
+    if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, DP_ACT_NONE>), grid, dim3(512), 0, s, p); \
+    else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, DP_ACT_RELU>), grid, dim3(512), 0, s, p); \
+    else if (ea == DP_ACT_GELU) hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, DP_ACT_GELU>), grid, dim3(512), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_8ph_kernel<K_, C_, R_, -1>), grid, dim3(512), 0, s, p); } while (0)
   if (conv && p.relu_a) DP_8PH(true, true);
   else if (conv) DP_8PH(true, false);
   else if (p.relu_a) DP_8PH(false, true);
@@ -1840,16 +1907,21 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   dim3 grid(p.tiles_n * p.tiles_m);
   // the load-free epilogue for launches without per-row operands (needs_rowld), on the BK = 64
   // engines the planner picks; debug 1 << 20: always the general one (A/B)
-  const bool rl = needs_rowld(p) || (p.dbg & (1 << 20)) || BKT != 64;
+  const int ea = BKT == 64 ? fast_epi_act(p) : -1;
+#define DP_BIGE(C_, R_, E_) hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, C_, R_, 8, E_>), grid, dim3(NT_BIG), 0, s, p)
 #define DP_BIG(C_, R_) do { \
-    if (rl) hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, C_, R_, 8, true>), grid, dim3(NT_BIG), 0, s, p); \
-    else if constexpr (BKT == 64) hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, BKT, NS, PIPE, C_, R_, 8, false>), grid, dim3(NT_BIG), 0, s, p); \
+    if (ea < 0) DP_BIGE(C_, R_, -1); \
+    else if constexpr (BKT == 64) { \
+      if (ea == DP_ACT_NONE) DP_BIGE(C_, R_, DP_ACT_NONE); \
+      else if (ea == DP_ACT_RELU) DP_BIGE(C_, R_, DP_ACT_RELU); \
+      else DP_BIGE(C_, R_, DP_ACT_GELU); } \
   } while (0)
   if (conv && p.relu_a) DP_BIG(true, true);
   else if (conv) DP_BIG(true, false);
   else if (p.relu_a) DP_BIG(false, true);
   else DP_BIG(false, false);
 #undef DP_BIG
+#undef DP_BIGE
   DP_CHECK_LAUNCH();
   return 0;
 }

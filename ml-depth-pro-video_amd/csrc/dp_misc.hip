@@ -337,7 +337,9 @@ __global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW
 // algorithms (imgproc resize.cpp; restated in oracle/cv_resize_oracle.py): fixed-point bilinear
 // with 11-bit coefficients (SIMD vertical form, scalar form in the row tail), and area
 // averaging (integer-scale cells; fractional cell weights otherwise, float sums in table order,
-// no FMA contraction so that every rounding is OpenCV's).  One thread per output pixel.
+// no FMA contraction -- `fp contract(off)` on plain expressions: the __fmul_rn / __fadd_rn helpers
+// are plain operators that fuse after inlining -- so that every rounding is OpenCV's).  One
+// thread per output pixel.
 __device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v); }
 __device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
 
@@ -345,14 +347,14 @@ __device__ __forceinline__ void cv_lin_tap(int d, double scale, int n, bool clam
 #pragma clang fp contract(off)
   float f = (float)((d + 0.5) * scale - 0.5);
   int sidx = (int)floorf(f);
-  f = __fsub_rn(f, (float)sidx);
+  f = f - (float)sidx;
   if (clamp_index) {
     if (sidx < 0) { f = 0.f; sidx = 0; }
     if (sidx >= n - 1) { f = 0.f; sidx = n - 1; }
   }
   i0 = sidx;
-  w0 = cv_round(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
-  w1 = cv_round(__fmul_rn(f, 2048.f));
+  w0 = cv_round((1.f - f) * 2048.f);
+  w1 = cv_round(f * 2048.f);
 }
 
 // one axis of computeResizeAreaTab for output index d: visits (source index, alpha) in table order
@@ -409,7 +411,7 @@ __global__ void __launch_bounds__(256) cv_resize_kernel(const uint8_t* __restric
     for (int c = 0; c < 3; ++c) {
       int v;
       if (isx == 2 && isy == 2 && dx < tail0) v = (sum[c] + 2) >> 2;     // SIMD form of the 2 x 2 cells
-      else v = cv_round(__fmul_rn((float)sum[c], sc));
+      else v = cv_round((float)sum[c] * sc);
       o[c] = sat_u8(v);
     }
   } else {
@@ -419,10 +421,10 @@ __global__ void __launch_bounds__(256) cv_resize_kernel(const uint8_t* __restric
       const uint8_t* r = src + (long long)sy * W * 3;
       cv_area_taps(dx, scale_x, W, [&](int sx, float alpha) {
         #pragma unroll
-        for (int c = 0; c < 3; ++c) buf[c] = __fadd_rn(buf[c], __fmul_rn((float)r[sx * 3 + c], alpha));
+        for (int c = 0; c < 3; ++c) buf[c] = buf[c] + (float)r[sx * 3 + c] * alpha;
       });
       #pragma unroll
-      for (int c = 0; c < 3; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(beta, buf[c]));
+      for (int c = 0; c < 3; ++c) acc[c] = acc[c] + beta * buf[c];
     });
     #pragma unroll
     for (int c = 0; c < 3; ++c) o[c] = sat_u8(cv_round(acc[c]));
