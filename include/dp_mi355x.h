@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 7
+#define DP_ABI_VERSION 8
 int dp_abi_version(void);
 
 /*
@@ -133,6 +133,16 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 
 /*
+ * dp_gemm_grouped: `groups` (1..4) dp_gemm problems in ONE launch.  args[0..groups-1] must agree
+ * in every field but the operand pointers A, B, bias, gamma, pos, R1, R2 and C (dense A, row
+ * stores, no fused head); each problem gives exactly the result its own dp_gemm call would
+ * (the 256 x 128 big engine; the tile hint is ignored).  Replaces the image encoder's and the FOV
+ * encoder's ViT Linears / patch embeds -- two ViT-L with their own weights over the same x2 input
+ * (encoder.py:308-311, fov.py:66-72) -- run side by side as one workgroup range per problem.
+ */
+int dp_gemm_grouped(const dp_gemm_args* args, int32_t groups, dp_stream_t stream);
+
+/*
  * Bytes of workspace the stream-K engine needs (flags + one fp32 256x256 partial
  * tile per persistent workgroup).  The caller zeroes it once after allocation; every
  * hand-off flag a stream-K launch sets is reset by the workgroup that consumes it, so
@@ -171,6 +181,15 @@ int dp_gemm_plan(const dp_gemm_args* args, int32_t* tile, int32_t* grid);
  */
 int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy,
                  int32_t rows, int32_t cols, float eps, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_layernorm_grouped: dp_layernorm over groups * rows_per_group rows, rows of group g taking
+ * w[g] / b[g] (w, b: HOST arrays of `groups` (1..4) device pointers) -- the image and FOV
+ * encoders' norm1 / norm2 / final norm in one launch.
+ */
+int dp_layernorm_grouped(const float* x, int64_t ldx, const float* const* w, const float* const* b,
+                         int32_t groups, void* y, int64_t ldy, int32_t rows_per_group, int32_t cols,
+                         float eps, int32_t dtype, dp_stream_t stream);
 
 /*
  * dp_attention: multi-head softmax attention, flash-style (no S x S in HBM).

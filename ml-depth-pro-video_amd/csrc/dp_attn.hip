@@ -74,9 +74,18 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
 // Measured and rejected (round 2): software-prefetched fragments (3 workgroups per CU), a
 // 3-deep K/V ring, packed row-sum adds, row sums on the matrix core (profiles/r02l_attn_pf/,
 // r02z6_attn_nst3/, r02p_attn_sadd/).
+// Ablation build only (make attnexp: -DDP_ATTN_ABLATE, tools/attn_bench.py --ablate): `dbg` bits
+// drop one stage each (outputs invalid) -- 1 the exp2, 2 the P.V MFMAs, 4 the per-tile wait +
+// barrier, 8 the K/V LDS-DMA (and the wait), 16 the row-sum adds.  The product build ignores it.
+#ifdef DP_ATTN_ABLATE
+#define ABL(b) (dbg & (b))
+#else
+#define ABL(b) false
+#endif
+
 template <typename K_, bool PRE>
 __global__ void __launch_bounds__(256, 4)
-attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2) {
+attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2, int dbg) {
   __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
   auto stage_of = [](int t) { return t & 1; };
   __shared__ int redo;
@@ -121,6 +130,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   const int prow = wave * 8 + (lane >> 3), pslot = lane & 7;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(&smem[0][0]) + wave * 1024);
   auto issue = [&](int k0, int buf) __attribute__((always_inline)) {
+    if (ABL(8)) return;
     const uint32_t dk = __builtin_amdgcn_readfirstlane(lds0 + buf * 2 * TILE_B), dv = dk + TILE_B;
     #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -207,7 +217,10 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         float p0, p1;
-        if (off) {
+        if (ABL(1)) {
+          p0 = s[8 * st + 2 * jj];
+          p1 = s[8 * st + 2 * jj + 1];
+        } else if (off) {
           p0 = __builtin_amdgcn_exp2f(s[8 * st + 2 * jj]);
           p1 = __builtin_amdgcn_exp2f(s[8 * st + 2 * jj + 1]);
         } else {
@@ -215,9 +228,14 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
           p1 = __builtin_amdgcn_exp2f(fmaf(s[8 * st + 2 * jj + 1], sl2, -m_run));
         }
         w[jj] = K_::pack2(p0, p1);
-        ls4[0] = (ls4[0] + p0) + p1;
+        if (!ABL(16)) ls4[0] = (ls4[0] + p0) + p1;
       }
       pf[st] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    if (ABL(2)) {   // keep P live without the P.V stage
+      asm volatile("" ::"v"(pf[0].x), "v"(pf[0].y), "v"(pf[0].z), "v"(pf[0].w), "v"(pf[1].x), "v"(pf[1].y),
+                   "v"(pf[1].z), "v"(pf[1].w));
+      return;
     }
     #pragma unroll
     for (int st = 0; st < 2; ++st) {
@@ -300,7 +318,7 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     // top of tile t: tile t landed (own pieces: vmcnt(0); everyone's: the barrier, which also
     // frees the stage of tile t-1 for the next issue)
     auto top = [&](int t) __attribute__((always_inline)) {
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      if (!ABL(4) && !ABL(8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
       if (t + 1 < nmma) issue((t + 1) * KT, stage_of(t + 1));
     };
     if (nfull > 0) {
@@ -365,6 +383,8 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
 }  // namespace
 
 namespace {
+int g_attn_dbg = 0;   // ablation build: dp_attn_debug_flags
+
 int attention_launch(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads, int32_t head_dim,
                      float scale, bool pre, int32_t dtype, dp_stream_t stream) {
   if (!qkv || !out) return DP_ERR_ARG;
@@ -380,16 +400,23 @@ int attention_launch(const void* qkv, void* out, int32_t batch, int32_t seq, int
   hipStream_t s = (hipStream_t)stream;
   if (dtype != DP_BF16 && dtype != DP_F16) return DP_ERR_DTYPE;
   if (pre) {
-    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-    else hipLaunchKernelGGL((attn_kernel<KF16, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2, g_attn_dbg);
+    else hipLaunchKernelGGL((attn_kernel<KF16, true>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2, g_attn_dbg);
   } else {
-    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
-    else hipLaunchKernelGGL((attn_kernel<KF16, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2);
+    if (dtype == DP_BF16) hipLaunchKernelGGL((attn_kernel<KBF16, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2, g_attn_dbg);
+    else hipLaunchKernelGGL((attn_kernel<KF16, false>), grid, dim3(256), 0, s, (const u16*)qkv, (u16*)out, seq, heads, nq, sl2, g_attn_dbg);
   }
   DP_CHECK_LAUNCH();
   return 0;
 }
 }  // namespace
+
+#ifdef DP_ATTN_ABLATE
+extern "C" int dp_attn_debug_flags(int flags) {
+  g_attn_dbg = flags;
+  return 0;
+}
+#endif
 
 extern "C" int dp_attention(const void* qkv, void* out, int32_t batch, int32_t seq, int32_t heads,
                             int32_t head_dim, float scale, int32_t dtype, dp_stream_t stream) {

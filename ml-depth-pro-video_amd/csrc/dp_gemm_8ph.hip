@@ -1,0 +1,8 @@
+// dp_gemm_8ph.hip: the 8-phase 256 x 256 engine.
+#include "dp_gemm_impl.h"
+
+namespace dpg {
+int launch_part_8ph(const GemmP& p, int, bool conv, bool bf16, hipStream_t s) {
+  return (bf16 ? launch_8ph<KBF16>(p, conv, s) : launch_8ph<KF16>(p, conv, s));
+}
+}  // namespace dpg

@@ -11,15 +11,26 @@ namespace {
 // fp32 (timm nn.LayerNorm(eps=1e-6)), 16-bit output.  Lane l owns the 8
 // consecutive columns 8 l + 512 j (j < VEC / 2): two 16-B loads per group and ONE
 // 16-B store (a full 1 KiB line set per wave-instruction; 8-B stores wrote half).
+// Affine parameters per row group (dp_layernorm_grouped: rows [g * rpg, (g + 1) * rpg) take
+// w[g] / b[g]; dp_layernorm: one group).
+constexpr int LN_MAX_GROUPS = 4;
+struct LnW {
+  const float* w[LN_MAX_GROUPS];
+  const float* b[LN_MAX_GROUPS];
+  int rpg;
+};
+
 template <typename K_, int VEC>
-__global__ void __launch_bounds__(256) ln_kernel(const float* __restrict__ x, long long ldx,
-                                                 const float* __restrict__ w, const float* __restrict__ b,
+__global__ void __launch_bounds__(256) ln_kernel(const float* __restrict__ x, long long ldx, const LnW lw,
                                                  u16* __restrict__ y, long long ldy, int rows, float eps) {
   static_assert(VEC % 2 == 0, "8 columns per lane");
   constexpr int G = VEC / 2;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (row >= rows) return;
+  const int grp = row / lw.rpg;
+  const float* __restrict__ w = lw.w[grp];
+  const float* __restrict__ b = lw.b[grp];
   constexpr int COLS = VEC * 256;
   const float* xr = x + (long long)row * ldx;
   float4 v[VEC];
@@ -66,12 +77,14 @@ __global__ void __launch_bounds__(256) ln_kernel(const float* __restrict__ x, lo
 
 // 256 columns: one float4 per lane, 8-B stores
 template <typename K_>
-__global__ void __launch_bounds__(256) ln256_kernel(const float* __restrict__ x, long long ldx,
-                                                    const float* __restrict__ w, const float* __restrict__ b,
+__global__ void __launch_bounds__(256) ln256_kernel(const float* __restrict__ x, long long ldx, const LnW lw,
                                                     u16* __restrict__ y, long long ldy, int rows, float eps) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   if (row >= rows) return;
+  const int grp = row / lw.rpg;
+  const float* __restrict__ w = lw.w[grp];
+  const float* __restrict__ b = lw.b[grp];
   const float4 v = *(const float4*)(x + (long long)row * ldx + lane * 4);
   float s = (v.x + v.y) + (v.z + v.w);
   #pragma unroll
@@ -91,14 +104,14 @@ __global__ void __launch_bounds__(256) ln256_kernel(const float* __restrict__ x,
 }
 
 template <typename K_>
-int ln_launch(const float* x, long long ldx, const float* w, const float* b, u16* y, long long ldy,
+int ln_launch(const float* x, long long ldx, const LnW& lw, u16* y, long long ldy,
               int rows, int cols, float eps, hipStream_t s) {
   dim3 grid((rows + 3) / 4);
   switch (cols) {
-    case 256: hipLaunchKernelGGL((ln256_kernel<K_>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
-    case 512: hipLaunchKernelGGL((ln_kernel<K_, 2>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
-    case 1024: hipLaunchKernelGGL((ln_kernel<K_, 4>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
-    case 2048: hipLaunchKernelGGL((ln_kernel<K_, 8>), grid, dim3(256), 0, s, x, ldx, w, b, y, ldy, rows, eps); break;
+    case 256: hipLaunchKernelGGL((ln256_kernel<K_>), grid, dim3(256), 0, s, x, ldx, lw, y, ldy, rows, eps); break;
+    case 512: hipLaunchKernelGGL((ln_kernel<K_, 2>), grid, dim3(256), 0, s, x, ldx, lw, y, ldy, rows, eps); break;
+    case 1024: hipLaunchKernelGGL((ln_kernel<K_, 4>), grid, dim3(256), 0, s, x, ldx, lw, y, ldy, rows, eps); break;
+    case 2048: hipLaunchKernelGGL((ln_kernel<K_, 8>), grid, dim3(256), 0, s, x, ldx, lw, y, ldy, rows, eps); break;
     default: return DP_ERR_SHAPE;
   }
   DP_CHECK_LAUNCH();
@@ -443,8 +456,32 @@ extern "C" int dp_layernorm(const float* x, int64_t ldx, const float* w, const f
   if (rows <= 0 || ldx % 4 || ldy % 4) return DP_ERR_SHAPE;
   if (cols > 256 && (ldy % 8 || (uintptr_t)y % 16)) return DP_ERR_ALIGN;   // 16-B row stores
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == DP_BF16) return ln_launch<KBF16>(x, ldx, w, b, (u16*)y, ldy, rows, cols, eps, s);
-  if (dtype == DP_F16) return ln_launch<KF16>(x, ldx, w, b, (u16*)y, ldy, rows, cols, eps, s);
+  LnW lw{};
+  lw.w[0] = w;
+  lw.b[0] = b;
+  lw.rpg = rows;
+  if (dtype == DP_BF16) return ln_launch<KBF16>(x, ldx, lw, (u16*)y, ldy, rows, cols, eps, s);
+  if (dtype == DP_F16) return ln_launch<KF16>(x, ldx, lw, (u16*)y, ldy, rows, cols, eps, s);
+  return DP_ERR_DTYPE;
+}
+
+extern "C" int dp_layernorm_grouped(const float* x, int64_t ldx, const float* const* w, const float* const* b,
+                                    int32_t groups, void* y, int64_t ldy, int32_t rows_per_group, int32_t cols,
+                                    float eps, int32_t dtype, dp_stream_t stream) {
+  if (!x || !w || !b || !y || groups < 1 || groups > LN_MAX_GROUPS) return DP_ERR_ARG;
+  if (rows_per_group <= 0 || ldx % 4 || ldy % 4) return DP_ERR_SHAPE;
+  if (cols > 256 && (ldy % 8 || (uintptr_t)y % 16)) return DP_ERR_ALIGN;
+  LnW lw{};
+  for (int g = 0; g < groups; ++g) {
+    if (!w[g] || !b[g]) return DP_ERR_ARG;
+    lw.w[g] = w[g];
+    lw.b[g] = b[g];
+  }
+  lw.rpg = rows_per_group;
+  const int rows = groups * rows_per_group;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DP_BF16) return ln_launch<KBF16>(x, ldx, lw, (u16*)y, ldy, rows, cols, eps, s);
+  if (dtype == DP_F16) return ln_launch<KF16>(x, ldx, lw, (u16*)y, ldy, rows, cols, eps, s);
   return DP_ERR_DTYPE;
 }
 

@@ -22,7 +22,7 @@ DP_CV_INTER_LINEAR, DP_CV_INTER_AREA = 1, 3
  DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
  DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128) = range(18)
-DP_ABI_VERSION = 7
+DP_ABI_VERSION = 8
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -32,7 +32,8 @@ LIB_PATH = os.environ.get(
 
 # (name, ctypes type) in header order
 EXPORTS = (
-    "dp_abi_version", "dp_gemm", "dp_layernorm", "dp_attention", "dp_attention_log2q", "dp_normalize_u8",
+    "dp_abi_version", "dp_gemm", "dp_gemm_grouped", "dp_layernorm", "dp_layernorm_grouped", "dp_attention",
+    "dp_attention_log2q", "dp_normalize_u8",
     "dp_resize_bilinear", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
     "dp_merge_windows_range", "dp_fov_tail", "dp_infer_epilogue", "dp_gemm_workspace_size", "dp_gemm_plan",
     "dp_depth_to_points", "dp_gemm_workspace_check", "dp_resize_u8_cv",
@@ -94,6 +95,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     sig = {
         "dp_abi_version": [],
         "dp_gemm": [ctypes.POINTER(GemmArgs), vp],
+        "dp_gemm_grouped": [ctypes.POINTER(GemmArgs), i32, vp],
+        "dp_layernorm_grouped": [vp, i64, vp, vp, i32, vp, i64, i32, i32, f32, i32, vp],
         "dp_layernorm": [vp, i64, vp, vp, vp, i64, i32, i32, f32, i32, vp],
         "dp_attention": [vp, vp, i32, i32, i32, i32, f32, i32, vp],
         "dp_attention_log2q": [vp, vp, i32, i32, i32, i32, i32, vp],

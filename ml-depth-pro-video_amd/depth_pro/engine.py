@@ -27,7 +27,7 @@ from ._lib import DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DPError, lo
 from .spec import DEPTH, EMBED_DIM, HEADS, IMG_SIZE, MLP_DIM, TOKENS
 
 # Timing ablations for tools/frame_ablation.py only (results are wrong when set):
-# comma list of {side, img, fovenc, attn, ln, vitgemm, decoder, head}.
+# comma list of {side, attn, ln, vitgemm, decoder, head}.
 _ABLATE = set(filter(None, os.environ.get("DP_ABLATE", "").split(",")))
 
 NWIN = 35
@@ -221,6 +221,15 @@ class _ViTBuffers:
         self.out = self.h if out_dt == dt else self.a.view(out_dt)
 
 
+class _ViTRows:
+    """Rows [lo, hi) of a _ViTBuffers (one encoder of the grouped side pair)."""
+
+    def __init__(self, buf: _ViTBuffers, lo: int, hi: int):
+        self.rows = hi - lo
+        self.x = buf.x[lo:hi]
+        self.out = buf.out[lo:hi]
+
+
 class FrameStatus:
     """Health of ONE forward, read without stalling the stream that ran it.
 
@@ -263,8 +272,9 @@ class Engine:
     """One frame (batch 1) per forward; static workspace (~4 GB).
 
     Streams (`_forward`): the main stream runs patchify -> patch encoder -> merges -> decoder ->
-    head; `side` runs the image encoder and `side2` the FOV encoder beside the patch encoder
-    (M = 577 rows each: far too few tiles to fill the chip alone); after the patch encoder the
+    head; `side` runs the image and FOV encoders beside the patch encoder, as ONE grouped ViT
+    (M = 577 rows each: far too few tiles to fill the chip alone, and paired, half the launches
+    with twice the workgroups each); after the patch encoder the
     project/upsample chains run on `dec_a` / `dec_b` and the decoder's encoder-feature projections,
     the lat0 chain's last deconv and the FOV head on `dec_c`, beside the main stream's decoder.
     At most four streams carry work at any time (HIP's default of four hardware queues per
@@ -293,8 +303,11 @@ class Engine:
         self.x0 = e(3, S, S, dtype=torch.float32)           # network input (normalized, 1536^2)
         self.cols = e(NWIN * PTOK, 768, dtype=vdt)
         self.vp = _ViTBuffers(NWIN * TOK, vdt, dev, dt)     # patch encoder (35 windows)
-        self.vi = _ViTBuffers(TOK, vdt, dev, dt)            # image encoder
-        self.vf = _ViTBuffers(TOK, vdt, dev, dt) if self.use_fov else None
+        # image + FOV encoders, run as one grouped ViT (rows 0..576 image, 577..1153 FOV)
+        self.side_vits = ["encoder.image_encoder."] + (["fov.encoder.0."] if self.use_fov else [])
+        self.vs = _ViTBuffers(len(self.side_vits) * TOK, vdt, dev, dt)
+        self.vi = _ViTRows(self.vs, 0, TOK)
+        self.vf = _ViTRows(self.vs, TOK, 2 * TOK) if self.use_fov else None
         # merged encoder maps (NHWC)
         self.lat0 = e(96 * 96, D)
         self.lat1 = e(96 * 96, D)
@@ -334,8 +347,7 @@ class Engine:
         self.f6 = e(6 * 6, 32)
         self.fov_deg = e(1, 1, 1, 1, dtype=torch.float32)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
-        self.side = torch.cuda.Stream(device=dev)      # image encoder
-        self.side2 = torch.cuda.Stream(device=dev)     # FOV encoder
+        self.side = torch.cuda.Stream(device=dev)      # image + FOV encoders (grouped)
         self.dec_a = torch.cuda.Stream(device=dev)     # lat0 project/upsample chain
         self.dec_b = torch.cuda.Stream(device=dev)     # f1 / f0 / lat1 chains
         self.dec_c = torch.cuda.Stream(device=dev)     # decoder projections, lat0's last deconv, FOV head
@@ -361,38 +373,60 @@ class Engine:
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
 
     # ------------------------------------------------------------------ ViT
-    def _vit(self, pre: str, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
+    def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
         """timm forward_features (vit_factory.py:97-99 -> vision_transformer.py): patch embed + cls /
-        pos, 24 Blocks, final norm; `hooks[i]()` runs after block i (encoder.py:133-144)."""
+        pos, 24 Blocks, final norm; `hooks[i]()` runs after block i (encoder.py:133-144).
+
+        `pres`: the weight prefixes of G ViTs of one shape over the same im2col rows (G = 2: the
+        image and FOV encoders, encoder.py:308-311 and fov.py:66-72); ViT g owns rows
+        [g * n_img * 577, (g + 1) * n_img * 577) of `buf`, and every op runs as ONE grouped launch
+        for the G of them (dp_gemm_grouped / dp_layernorm_grouped, attention over G * n_img)."""
         P, M = self.P, n_img * TOK
+        G = len(pres)
+        ln_on, gemm_on = "ln" not in _ABLATE, "vitgemm" not in _ABLATE
+
+        def lin(A, key, C, N, K, a_rows=True, **kw):
+            """The G problems' `key` Linear: A rows / C rows of problem g at g * M (A shared when
+            not a_rows); per-problem bias / gamma / pos given as key suffixes in kw."""
+            per = {k: kw.pop(k) for k in ("bias", "gamma", "pos") if isinstance(kw.get(k), str)}
+            A_off = kw.pop("A_off", 0)
+            groups = []
+            for g, pre in enumerate(pres):
+                d = dict(A=A, B=P[pre + key], C=C, A_off=A_off + (g * M * K if a_rows else 0), C_off=g * M * N)
+                d.update({k: P[pre + v] for k, v in per.items()})
+                groups.append(d)
+            ops.gemm_grouped(groups, M=kw.pop("M", M), N=N, K=K, **kw)
+
+        def norm(key, out):
+            ops.layernorm_grouped(buf.x, [P[pre + key + ".weight"] for pre in pres],
+                                  [P[pre + key + ".bias"] for pre in pres], out, M, D)
+
         # patch embed (k16 s16 conv as GEMM over the im2col rows) + bias + pos -> rows 1..576
-        ops.gemm(self.cols, P[pre + "pe.w"], buf.x, M=n_img * PTOK, N=D, K=768,
-                 A_off=cols_off_rows * 768, bias=P[pre + "pe.b"], pos=P[pre + "pos"], ldpos=D,
-                 pos_group=PTOK, pos_off=1, row_group=PTOK, row_group_out=TOK, row_off=1)
-        ops.vit_cls_rows(buf.x, P[pre + "cls"], P[pre + "pos"], n_img)
-        ln, gemm = "ln" not in _ABLATE, "vitgemm" not in _ABLATE
+        lin(self.cols, "pe.w", buf.x, D, 768, a_rows=False, M=n_img * PTOK, A_off=cols_off_rows * 768,
+            bias="pe.b", pos="pos", ldpos=D, pos_group=PTOK, pos_off=1, row_group=PTOK, row_group_out=TOK,
+            row_off=1)
+        for g, pre in enumerate(pres):
+            ops.vit_cls_rows(buf.x[g * M:], P[pre + "cls"], P[pre + "pos"], n_img)
         for i in range(DEPTH):
-            b = f"{pre}blocks.{i}."
-            if ln:
-                ops.layernorm(buf.x, P[b + "norm1.weight"], P[b + "norm1.bias"], buf.h, M, D)
-            if gemm:
-                ops.gemm(buf.h, P[b + "attn.qkv.weight"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.bias"],
-                         gamma=self.qkv_gamma)
+            b = f"blocks.{i}."
+            if ln_on:
+                norm(b + "norm1", buf.h)
+            if gemm_on:
+                lin(buf.h, b + "attn.qkv.weight", buf.qkv, 3 * D, D, bias=b + "attn.qkv.bias", gamma=self.qkv_gamma)
             if "attn" not in _ABLATE:
-                ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
-            if gemm:
-                ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
-                         gamma=P[b + "ls1.gamma"], accumulate=True)
-            if ln:
-                ops.layernorm(buf.x, P[b + "norm2.weight"], P[b + "norm2.bias"], buf.h, M, D)
-            if gemm:
-                ops.gemm(buf.h, P[b + "mlp.fc1.weight"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.bias"],
-                         act=DP_ACT_GELU)
-                ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
-                         gamma=P[b + "ls2.gamma"], accumulate=True)
+                ops.attention(buf.qkv, buf.a, G * n_img, TOK, HEADS, D // HEADS, log2q=True)
+            if gemm_on:
+                lin(buf.a, b + "attn.proj.weight", buf.x, D, D, bias=b + "attn.proj.bias", gamma=b + "ls1.gamma",
+                    accumulate=True)
+            if ln_on:
+                norm(b + "norm2", buf.h)
+            if gemm_on:
+                lin(buf.h, b + "mlp.fc1.weight", buf.m, MLP_DIM, D, bias=b + "mlp.fc1.bias", act=DP_ACT_GELU)
+                lin(buf.m, b + "mlp.fc2.weight", buf.x, D, MLP_DIM, bias=b + "mlp.fc2.bias", gamma=b + "ls2.gamma",
+                    accumulate=True)
             if hooks and i in hooks:
                 hooks[i]()
-        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
+        norm("norm", buf.out)
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
@@ -433,19 +467,16 @@ class Engine:
         return self.feats
 
     # -------------------------------------------------------------- encoders
-    def _image_encoder(self):
-        """Image encoder ViT on x2 (encoder.py:308-311) + the lowres upsample into `cat`."""
+    def _side_encoders(self):
+        """Image encoder ViT on x2 (encoder.py:308-311) and FOV encoder ViT (fov.py:66-72) as one
+        grouped ViT, then the lowres upsample into `cat` and the FOV Linear (fov.py:45-47)."""
         P, e = self.P, "encoder."
-        self._vit("encoder.image_encoder.", self.vi, 1, 34 * PTOK)
+        self._vit(self.side_vits, self.vs, 1, 34 * PTOK)
         ops.merge_windows(self.vi.out, 0, 1, 0, self.g)
         self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
                      C_off=D, ldc=2 * D)
-
-    def _fov_encoder(self):
-        """FOV encoder ViT + Linear (fov.py:45-47, 66-72)."""
-        vf, P = self.vf, self.P
-        self._vit("fov.encoder.0.", vf, 1, 34 * PTOK)
-        ops.gemm(vf.out, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
+        if self.use_fov:
+            ops.gemm(self.vf.out, P["fov.lin.w"], self.fov_tok, M=PTOK, N=128, K=D, A_off=D, bias=P["fov.lin.b"])
 
     def _fov_head(self):
         """FOV head (fov.py:56-82): needs the low-res decoder features and the FOV tokens."""
@@ -493,20 +524,15 @@ class Engine:
 
         # pyramid + 35 windows + patch-embed im2col (encoder.py:151-263)
         ops.patchify_pyramid(self.x0, self.cols)
-        # image and FOV encoders beside the patch encoder (M = 577 rows each)
+        # image and FOV encoders (one grouped ViT, M = 2 x 577 rows) beside the patch encoder
         if side_ok:
             with self._on(self.side):
-                if "img" not in _ABLATE:
-                    self._image_encoder()
-            if self.use_fov:
-                with self._on(self.side2):
-                    if "fovenc" not in _ABLATE:
-                        self._fov_encoder()
+                self._side_encoders()
         # patch encoder; hooks after blocks 5 / 11 (encoder.py:133-144, 267-288)
         vp = self.vp
         hooks = {5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
                  11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1)}
-        self._vit("encoder.patch_encoder.", vp, NWIN, 0, hooks)
+        self._vit(["encoder.patch_encoder."], vp, NWIN, 0, hooks)
         ops.merge_windows(vp.out, 0, 5, 3, self.f0)
         ops.merge_windows(vp.out, 25, 3, 6, self.f1)
         ops.merge_windows(vp.out, 34, 1, 0, self.f2)
@@ -555,7 +581,7 @@ class Engine:
             ev["enc0"] = mark(self.dec_c)
             if self.use_fov and side_ok:
                 if not serial:
-                    self.dec_c.wait_stream(self.side2)
+                    self.dec_c.wait_stream(self.side)
                 self._fov_head()
         if "decoder" not in _ABLATE:
             f = self._fusion(4, self.low, 48, None)
@@ -569,7 +595,7 @@ class Engine:
         else:
             feats = self.feats
         if not serial:
-            for st in (self.dec_a, self.dec_b, self.dec_c, self.side2):
+            for st in (self.dec_a, self.dec_b, self.dec_c, self.side):
                 main.wait_stream(st)
         if "head" in _ABLATE:
             return self.canonical, self.fov_deg
@@ -625,10 +651,20 @@ class Engine:
         return st
 
     def check_status(self, block: bool = True) -> None:
-        """Raise DPError if one of the recent frames is bad (block=False: only frames already done)."""
+        """Raise DPError if one of the recent frames not checked yet is bad (block=False: only
+        frames already done).  Each frame's status is reported once: checked frames leave the
+        list, so a bad frame does not fail every later check."""
+        keep = []
+        bad = None
         for st in self._recent:
             if block or st.ready():
-                st.check()
+                if bad is None and st.error() is not None:
+                    bad = st
+            else:
+                keep.append(st)
+        self._recent = keep
+        if bad is not None:
+            bad.check()
 
 
 class _StreamCtx:

@@ -149,6 +149,44 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     `workspace` (or the one set by `use_workspace`) enables the stream-K engine.
     `plan_only=True` launches nothing and returns (tile, workgroups) from dp_gemm_plan.
     """
+    a = _gemm_args(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc, conv=conv, relu_a=relu_a, bias=bias,
+                   act=act, gamma=gamma, pos=pos, ldpos=ldpos, pos_group=pos_group, pos_off=pos_off, R1=R1,
+                   ldr1=ldr1, R2=R2, ldr2=ldr2, accumulate=accumulate, deconv=deconv, row_group=row_group,
+                   row_group_out=row_group_out, row_off=row_off, head_w=head_w, head_b=head_b,
+                   head_corr=head_corr, A_off=A_off, C_off=C_off, B_off=B_off, tile=tile, workspace=workspace,
+                   border_corr=border_corr)
+    if plan_only:
+        t, g = ctypes.c_int32(), ctypes.c_int32()
+        check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
+        return t.value, g.value
+    _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None, B_off)
+    kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
+    with _Timed(kind, 2.0 * M * N * K, (M, N, K), B.dtype):
+        check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
+
+
+def gemm_grouped(groups, **common) -> None:
+    """dp_gemm_grouped: len(groups) dense GEMMs of one shape in one launch.  Each entry of `groups`
+    is a dict with that problem's tensors -- A, B, C and optionally bias, gamma, pos, R1, R2 and the
+    element offsets A_off / C_off -- and `common` holds the shared arguments of `gemm` (M, N, K,
+    act, accumulate, row_group, ...).  Same result as one `gemm` call per problem."""
+    arr = (GemmArgs * len(groups))()
+    for i, g in enumerate(groups):
+        kw = dict(common)
+        kw.update(g)
+        A, B, C = kw.pop("A"), kw.pop("B"), kw.pop("C")
+        arr[i] = _gemm_args(A, B, C, **kw)
+        _check_gemm_extents(A, B, C, arr[i], kw.get("A_off", 0), kw.get("C_off", 0), None, None, False, False)
+    M, N, K = common["M"], common["N"], common["K"]
+    with _Timed("gemm", 2.0 * M * N * K * len(groups), (M, N, K), groups[0]["B"].dtype):
+        check(_lib.load().dp_gemm_grouped(arr, len(groups), _stream(groups[0]["C"])), "dp_gemm_grouped")
+
+
+def _gemm_args(A, B, C, *, M, N, K, lda=None, ldb=None, ldc=None, conv=None, relu_a=False, bias=None,
+               act=DP_ACT_NONE, gamma=None, pos=None, ldpos=0, pos_group=0, pos_off=0, R1=None, ldr1=0, R2=None,
+               ldr2=0, accumulate=False, deconv=None, row_group=0, row_group_out=0, row_off=0, head_w=None,
+               head_b=0.0, head_corr=None, A_off=0, C_off=0, B_off=0, tile=0, workspace=None,
+               border_corr=None) -> "GemmArgs":
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.dtype = dtype_code(B.dtype)
@@ -194,14 +232,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     ws = workspace if workspace is not None else _WS
     if ws is not None:
         a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * ws.element_size()
-    if plan_only:
-        t, g = ctypes.c_int32(), ctypes.c_int32()
-        check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
-        return t.value, g.value
-    _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None, B_off)
-    kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
-    with _Timed(kind, 2.0 * M * N * K, (M, N, K), B.dtype):
-        check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
+    return a
 
 
 def _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head, head_ps, B_off=0) -> None:
@@ -236,6 +267,20 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor
     with _Timed("layernorm", 0.0, (rows, cols), y.dtype):
         check(_lib.load().dp_layernorm(x.data_ptr(), cols, w.data_ptr(), b.data_ptr(), y.data_ptr(), cols,
                                        rows, cols, eps, dtype_code(y.dtype), _stream(y)), "dp_layernorm")
+
+
+def layernorm_grouped(x: torch.Tensor, ws, bs, y: torch.Tensor, rows_per_group: int, cols: int,
+                      eps: float = 1e-6) -> None:
+    """dp_layernorm_grouped: rows [g * rows_per_group, (g + 1) * rows_per_group) normalised with
+    ws[g] / bs[g] -- one launch for several LayerNorms of one shape."""
+    n = len(ws)
+    pw = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ws])
+    pb = (ctypes.c_void_p * n)(*[t.data_ptr() for t in bs])
+    if x.numel() < n * rows_per_group * cols or y.numel() < n * rows_per_group * cols:
+        raise _lib.DPError("dp_layernorm_grouped: x / y smaller than groups * rows_per_group * cols")
+    with _Timed("layernorm", 0.0, (n * rows_per_group, cols), y.dtype):
+        check(_lib.load().dp_layernorm_grouped(x.data_ptr(), cols, pw, pb, n, y.data_ptr(), cols, rows_per_group,
+                                               cols, eps, dtype_code(y.dtype), _stream(y)), "dp_layernorm_grouped")
 
 
 def attention(qkv: torch.Tensor, out: torch.Tensor, batch: int, seq: int, heads: int = 16,

@@ -189,6 +189,79 @@ def test_layernorm(cuda, dt, cols):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("groups", [2, 3])
+def test_layernorm_grouped_matches_per_group(cuda, dt, groups):
+    """dp_layernorm_grouped (the side encoders' norms in one launch) = one dp_layernorm per group,
+    bit for bit, and each group uses its own affine parameters."""
+    g = torch.Generator().manual_seed(23)
+    R, cols = 577, 1024
+    x = (torch.randn(groups * R, cols, generator=g) * 2 - 1).to(cuda)
+    ws = [torch.randn(cols, generator=g).to(cuda) for _ in range(groups)]
+    bs = [torch.randn(cols, generator=g).to(cuda) for _ in range(groups)]
+    y = torch.empty(groups * R, cols, dtype=dt, device=cuda)
+    ops.layernorm_grouped(x, ws, bs, y, R, cols)
+    y1 = torch.empty_like(y)
+    for i in range(groups):
+        ops.layernorm(x[i * R:], ws[i], bs[i], y1[i * R:], R, cols)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y1)
+    close(y[R:2 * R], F.layer_norm(x[R:2 * R], (cols,), ws[1], bs[1], 1e-6), dt, "layernorm group 1")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("case", ["qkv", "proj", "fc1", "fc2", "patch"])
+def test_gemm_grouped_bit_identical_to_single(cuda, dt, case):
+    """dp_gemm_grouped (the image + FOV encoders' Linears / patch embed as one launch) gives each
+    problem exactly what its own dp_gemm call gives -- same engine, same epilogue -- and each
+    problem reads its own weights / bias / gamma / pos."""
+    g = torch.Generator().manual_seed(11)
+    N, K = {"qkv": (3072, 1024), "proj": (1024, 1024), "fc1": (4096, 1024), "fc2": (1024, 4096),
+            "patch": (1024, 768)}[case]
+    patch = case == "patch"
+    M, R = (576 if patch else 577), 577
+    A = rnd((1 if patch else 2) * M, K, dt=dt, dev=cuda, gen=g)
+    acc = case in ("proj", "fc2")
+    cdt = torch.float32 if acc or patch else dt
+    C0 = torch.randn(2 * R, N, generator=g).to(cdt).to(cuda)
+    kw = dict(M=M, N=N, K=K)
+    if case == "fc1":
+        kw["act"] = DP_ACT_GELU
+    if acc:
+        kw["accumulate"] = True
+    if patch:
+        kw.update(ldpos=N, pos_group=576, pos_off=1, row_group=576, row_group_out=577, row_off=1)
+    per = []
+    for i in range(2):
+        d = dict(A=A, B=rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5),
+                 bias=torch.randn(N, generator=g).to(cuda), A_off=0 if patch else i * M * K, C_off=i * R * N)
+        if case in ("qkv", "proj", "fc2"):
+            d["gamma"] = torch.rand(N, generator=g).to(cuda)
+        if patch:
+            d["pos"] = torch.randn(577, N, generator=g).to(cuda)
+        per.append(d)
+    Cg, Cs = C0.clone(), C0.clone()
+    ops.gemm_grouped([dict(d, C=Cg) for d in per], **kw)
+    for d in per:
+        ops.gemm(d["A"], d["B"], Cs, **{k: v for k, v in d.items() if k not in ("A", "B")}, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(Cg, Cs), (Cg.float() - Cs.float()).abs().max().item()
+    # problem 1 against fp32 torch (its own operands, not problem 0's)
+    d = per[1]
+    a = A.float()[d["A_off"] // K:d["A_off"] // K + M]
+    v = a @ d["B"].float().t() + d["bias"]
+    if case == "fc1":
+        v = F.gelu(v)
+    if "gamma" in d:
+        v = v * d["gamma"]
+    if patch:
+        v = v + d["pos"][1:]
+        ref, got = v, Cg[R + 1:2 * R]
+    else:
+        ref, got = v + (C0[R:2 * R].float() if acc else 0), Cg[R:2 * R]
+    close(got, ref, torch.float32 if (acc or patch) and dt == torch.float16 else dt, f"grouped {case}")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 def test_patchify_pyramid_vs_oracle_split(cuda, dt):
     from oracle import depth_pro_oracle as O
 

@@ -193,6 +193,10 @@ def test_engine_reports_stream_k_timeout_on_its_frame(model):
     with pytest.raises(DPError, match=f"frame {s1.frame}"):
         s1.check()
     assert torch.equal(d0, d2)
+    # the engine-wide check reports the bad frame once, then it is consumed
+    with pytest.raises(DPError, match=f"frame {s1.frame}"):
+        m.engine().check_status(block=True)
+    m.engine().check_status(block=True)
 
 
 def test_config1_example_jpg_vs_reference(model, golden_dir):

@@ -28,16 +28,34 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="only the 35 x 577 bf16 case, no torch reference")
+    ap.add_argument("--log2q", action="store_true", help="time dp_attention_log2q (what the engine runs)")
+    ap.add_argument("--ablate", action="store_true",
+                    help="35 x 577 with each stage dropped in turn (needs the ablation build: make attnexp, "
+                         "DP_MI355X_LIB=.../libdp_mi355x_attnexp.so)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     H, hd = 16, 64
+    if args.ablate:
+        from depth_pro import _lib
+        lib = _lib.load()
+        batch, seq = 35, 577
+        qkv = torch.randn(batch * seq, 3 * H * hd, device=dev).to(torch.bfloat16)
+        out = torch.empty(batch * seq, H * hd, dtype=torch.bfloat16, device=dev)
+        flop = 4.0 * batch * H * seq * seq * hd
+        for flags, lab in ((0, "full"), (1, "no exp"), (16, "no row sums"), (17, "no exp+sums"), (2, "no PV"),
+                           (4, "no tile wait/barrier"), (8, "no K/V DMA"), (10, "no DMA+PV"), (15, "S MFMA only")):
+            lib.dp_attn_debug_flags(flags)
+            ms = timeit(lambda: ops.attention(qkv, out, batch, seq, H, hd, log2q=True))
+            print(f"{lab:22s} {ms*1e3:7.1f}us {flop/ms/1e9:6.1f}TF", flush=True)
+        lib.dp_attn_debug_flags(0)
+        return
     cases = ((35, 577),) if args.quick else ((35, 577), (1, 577), (8, 2048))
     for batch, seq in cases:
         for dt in ((torch.bfloat16,) if args.quick else (torch.bfloat16, torch.float16)):
             qkv = torch.randn(batch * seq, 3 * H * hd, device=dev).to(dt)
             out = torch.empty(batch * seq, H * hd, dtype=dt, device=dev)
             flop = 4.0 * batch * H * seq * seq * hd
-            ms = timeit(lambda: ops.attention(qkv, out, batch, seq, H, hd))
+            ms = timeit(lambda: ops.attention(qkv, out, batch, seq, H, hd, log2q=args.log2q))
             if args.quick:
                 print(f"b={batch} seq={seq} dp {ms*1e3:.1f}us {flop/ms/1e9:.1f}TF", flush=True)
                 continue
