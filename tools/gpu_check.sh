@@ -37,6 +37,14 @@ for S in $STEPS; do
       timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
         SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE --output-format csv \
         -d $OUT/pmc_sq2 -o pmc -- python3 tools/frame_once.py > $OUT/pmc_sq2.log 2>&1 ;;
+    gemm)
+      # GEMM engine micro-benchmarks: fc1 / sq4096 on the 8-phase and dual engines, with the no-store ablation
+      timeout -k 10 300 python -u tools/gemm_bench.py --tile 8ph256x256,dual256x128,big320x256 --only fc1 --ablate \
+        > $OUT/gemm_fc1.txt 2>&1
+      timeout -k 10 300 python -u tools/gemm_bench.py --tile 8ph256x256,big320x256 --only sq4096 --ablate \
+        > $OUT/gemm_sq4096.txt 2>&1
+      timeout -k 10 300 python -u tools/gemm_bench.py --tile big320x256,8ph256x256 --only + --ablate \
+        > $OUT/gemm_res.txt 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
   echo "step $S ok"
