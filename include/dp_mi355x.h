@@ -128,7 +128,8 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
        DP_TILE_BIG_256x128_K32 = 7, DP_TILE_8PH_256x256 = 8, DP_TILE_DEEP4_256x256 = 9,
        DP_TILE_DEEP5_256x256 = 10, DP_TILE_DEEP_256x128 = 11, DP_TILE_STREAMK_256x256 = 12,
        DP_TILE_BIG_320x256 = 13, DP_TILE_BIG_512x128 = 14, DP_TILE_PBIG_320x256 = 15,
-       DP_TILE_PBIG_256x256 = 16, DP_TILE_DUAL_256x128 = 17 };
+       DP_TILE_PBIG_256x256 = 16, DP_TILE_DUAL_256x128 = 17,
+       DP_TILE_P8PH_256x256 = 18 };
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 

@@ -31,7 +31,7 @@ int launch_tile(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s) {
     case DP_TILE_PBIG_320x256: case DP_TILE_PBIG_256x256: return launch_part_pbig(p, tile, conv, bf16, s);
     case DP_TILE_256x64: case DP_TILE_256x32: case DP_TILE_128x128: case DP_TILE_DUAL_256x128:
       return launch_part_small(p, tile, conv, bf16, s);
-    case DP_TILE_8PH_256x256: return launch_part_8ph(p, tile, conv, bf16, s);
+    case DP_TILE_8PH_256x256: case DP_TILE_P8PH_256x256: return launch_part_8ph(p, tile, conv, bf16, s);
     case DP_TILE_BIG_320x256: case DP_TILE_BIG_512x128: return launch_part_big320(p, tile, conv, bf16, s);
     default: return launch_part_big(p, tile, conv, bf16, s);
   }
@@ -191,6 +191,15 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     else if (dense_ok && tile == DP_TILE_BIG_256x256 && tiles256 >= 2 * ncu)
       tile = DP_TILE_PBIG_256x256;
   }
+  // the persistent 8-phase engine: dense, N % 256 == 0, K >= 128, the load-free epilogue with a
+  // 16-bit C and bounded buffer stores (A/B: debug 1 << 22 puts the 8-phase launches on it)
+  if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && (dbg & (1 << 22)))) {
+    const bool ok = a->a_mode == DP_A_DENSE && a->N % 256 == 0 && a->K >= 128 && c_bytes && a->c_dtype != DP_F32 &&
+                    a->store_mode == DP_STORE_ROWS && !a->R1 && !a->R2 && !a->pos && !a->accumulate &&
+                    !a->row_group && !a->head_w && !a->head_corr && !(dbg & (1 << 20));
+    if (tile == DP_TILE_P8PH_256x256 && !ok) return DP_ERR_ARG;
+    if (ok) tile = DP_TILE_P8PH_256x256;
+  }
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
   // the border-corrected composed conv exists in the 512 x 128 conv engine only
   if (a->store_mode == DP_STORE_ROWS && a->head_corr && tile != DP_TILE_BIG_512x128) return DP_ERR_ARG;
@@ -216,6 +225,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   p.dbg = dbg;
   p.c_bytes = c_bytes;
+  // tile-ticket queues of the persistent 8-phase engine (debug 1 << 23: static walk, A/B)
+  p.tq = (ws_ok && !(dbg & (1 << 23))) ? (unsigned*)((char*)a->workspace + TQ_BYTE_OFF) : nullptr;
   p.groups = 1;
   p.stagger_wg = 0;
   p.stagger_sleeps = 0;
@@ -243,7 +254,8 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
   }
   if (tile_out) *tile_out = tile;
   int grid = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-  if (tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) grid = grid < num_cus() ? grid : num_cus();
+  if (tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256 || tile == DP_TILE_P8PH_256x256)
+    grid = grid < num_cus() ? grid : num_cus();
   if (grid_out) *grid_out = tile == DP_TILE_STREAMK_256x256 ? sk_grid(p) : grid;
   return 0;
 }

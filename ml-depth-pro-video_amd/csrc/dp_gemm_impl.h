@@ -29,6 +29,7 @@
 
 #pragma once
 #include <atomic>
+#include <type_traits>
 
 namespace dpg {
 
@@ -69,6 +70,7 @@ struct GemmP {
   int stagger_wg, stagger_sleeps;   // 2-workgroup-per-CU engine: start stagger (debug 1 << 21)
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
   unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
+  unsigned* tq;      // persistent 8-phase engine: tile-ticket queues in the workspace (NULL: static walk)
   // dp_gemm_grouped: `groups` problems of one shape in one launch (workgroup range g * tiles_m *
   // tiles_n ... covers problem g, whose operand pointers are grp[g]); 1 otherwise
   int groups;
@@ -151,8 +153,9 @@ __device__ unsigned long long g_stamps[5 * 65536];
 #define DP_STAMP_SAVE(wg) do { } while (0)
 #endif
 
-// 16 zero bytes x 8: source of the implicit-conv zero padding for LDS-DMA loads
-__device__ __attribute__((aligned(16))) uint32_t g_zero_page[32];
+// 256 zero bytes: source of the implicit-conv zero padding for LDS-DMA loads and of the
+// persistent engine's absent column constants
+__device__ __attribute__((aligned(16))) uint32_t g_zero_page[64];
 
 __device__ __forceinline__ int lds_off(int row, int chunk) {  // element offset, 64-wide rows
   return row * BK + ((chunk ^ (row & 7)) << 3);
@@ -559,14 +562,15 @@ __device__ __forceinline__ void epilogue_mfma(const GemmP& p, f32x4_t (&acc)[FM]
     for (int fm = 0; fm < PF; ++fm)
       #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
-        float x[4];
-        #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[f0 + fm][fn][r] + bias[fn][r];
-          if constexpr (ACT == DP_ACT_RELU) v = fmaxf(v, 0.f);
-          else if constexpr (ACT == DP_ACT_GELU) v = gelu_erf(v);
-          x[r] = v * gam[fn][r];
+        // packed-f32 arithmetic on the lane's 4 columns (gelu_erf4): same values as per element
+        f32x4_t x = acc[f0 + fm][fn] + f32x4_t{bias[fn][0], bias[fn][1], bias[fn][2], bias[fn][3]};
+        if constexpr (ACT == DP_ACT_RELU) {
+          #pragma unroll
+          for (int r = 0; r < 4; ++r) x[r] = fmaxf(x[r], 0.f);
+        } else if constexpr (ACT == DP_ACT_GELU) {
+          x = gelu_erf4(x);
         }
+        x = x * f32x4_t{gam[fn][0], gam[fn][1], gam[fn][2], gam[fn][3]};
         const int row = fm * 16 + t;
         const int chunk = fn * 2 + (g >> 1);
         uint2 w;
@@ -1554,6 +1558,375 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
   else if (p.relu_a) DP_8PH(false, true);
   else DP_8PH(false, false);
 #undef DP_8PH
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+// ============================================ persistent 8-phase 256x256 engine
+// gemm_8ph_kernel's K loop run over the workgroup's whole tile list (tiles wgid, wgid + G,
+// ... of the band raster, G = min(tiles, CUs)) as ONE stream of K steps: the LDS-DMA of the
+// next tile's first K steps is issued by the same per-phase schedule as any other step, so
+// it is in flight (or landed) while this tile's epilogue runs, and there is no per-tile
+// dispatch, prologue or store drain.  At a tile boundary the next tile's second A tile is
+// issued BEFORE the epilogue's stores, so the counted wait that retires it (phase 3 of the
+// next tile's first step) can leave the stores draining: vmcnt counts loads, stores and
+// LDS-DMA together in issue order (MI355X_MICROARCH.md), and the epilogue issues exactly
+// ESTORES buffer stores per lane (every lane stores; rows past M / columns past N get an
+// out-of-range offset, dropped by the hardware), so the count is a compile-time constant.
+// The epilogue is the load-free MFMA-layout one (bias, activation, gamma; 16-bit C) staged
+// through a 4 KiB slab per wave beside the 128 KiB ring (160 KiB of LDS in all), so no LDS
+// the ring uses is touched.  Dense A only (the ViT's fc1 / qkv).  Requires K >= 128.
+// The wave's column constants (bias / gamma of its 64 columns) come from its LDS const slot
+// (filled by LDS-DMA with the tile's loads), so the epilogue issues no global load: hipcc
+// would put a vmcnt(0) in front of one -- a wait for every LDS-DMA in flight, i.e. the next
+// tile's first K steps.
+// Per-XCD tile-ticket queues of the persistent 8-phase engine (workspace bytes [2048, 3200):
+// 8 queue counters + an exit counter, 128 B apart).  Queue x hands out, round by round, the
+// tile positions [x*G/8, (x+1)*G/8) of each round of G tiles -- the XCD-contiguous placement
+// of the static walk -- and a workgroup whose own queue is empty takes from the next XCD's.
+// The last workgroup to finish resets the counters (graph-replay safe, no memset).
+constexpr int TQ_BYTE_OFF = 2048;
+constexpr int TQ_STRIDE = 32;   // uint32 words between counters
+__device__ __forceinline__ int tq_map(int G, int T, int x, unsigned k) {
+  const int c0 = x * G / 8, len = (x + 1) * G / 8 - c0;
+  if (len <= 0) return -1;
+  const long long t = (long long)(k / (unsigned)len) * G + c0 + (int)(k % (unsigned)len);
+  return t < T ? (int)t : -1;
+}
+// thread 0 only: tickets from queue home+q, home+q+1, ... until a valid tile or all 8 are empty
+__device__ __forceinline__ int tq_draw(unsigned* tq, int G, int T, int home, int& q) {
+  for (; q < 8; ++q) {
+    const int x = (home + q) & 7;
+    const unsigned k = __hip_atomic_fetch_add(tq + TQ_STRIDE * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t = tq_map(G, T, x, k);
+    if (t >= 0) return t;
+  }
+  return -1;
+}
+
+template <typename K_, int ACT, bool HG>
+__device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)[8][4], char* slab,
+                                                  const float* cst, int lane, int m_base, int n_base,
+                                                  __amdgpu_buffer_rsrc_t crs) {
+  constexpr int FM = 8, FN = 4, TN = 64, PF = 1, CH = TN / 8, RPI = 64 / CH;
+  const int t = lane & 15, g = lane >> 4;
+  f32x4_t bias[FN], gam[FN];
+  #pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    bias[fn] = *(const f32x4_t*)(cst + fn * 16 + 4 * g);
+    if constexpr (HG) gam[fn] = *(const f32x4_t*)(cst + 64 + fn * 16 + 4 * g);
+  }
+  #pragma unroll
+  for (int f0 = 0; f0 < FM; f0 += PF) {
+    #pragma unroll
+    for (int fm = 0; fm < PF; ++fm)
+      #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        // packed-f32 arithmetic (the 4 columns of a lane as one vector): same values as the
+        // scalar epilogue_mfma, half the VALU issue slots
+        f32x4_t x = acc[f0 + fm][fn] + bias[fn];
+        if constexpr (ACT == DP_ACT_RELU) {
+          #pragma unroll
+          for (int r = 0; r < 4; ++r) x[r] = fmaxf(x[r], 0.f);
+        } else if constexpr (ACT == DP_ACT_GELU) {
+          x = gelu_erf4(x);
+        }
+        if constexpr (HG) x = x * gam[fn];
+        const int row = fm * 16 + t;
+        const int chunk = fn * 2 + (g >> 1);
+        uint2 w;
+        w.x = K_::pack2(x[0], x[1]);
+        w.y = K_::pack2(x[2], x[3]);
+        *(uint2*)(slab + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4) + (g & 1) * 8) = w;
+      }
+    #pragma unroll
+    for (int k = 0; k < PF * 16 / RPI; ++k) {
+      const int row = k * RPI + lane / CH, chunk = lane % CH;
+      const uint4 d = *(const uint4*)(slab + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4));
+      const int m = m_base + f0 * 16 + row, n = n_base + chunk * 8;
+      const unsigned bo = (m < p.M && n < p.N) ? (unsigned)(((long long)m * p.ldc + n) * 2) : p.c_bytes;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{d.x, d.y, d.z, d.w}, crs, bo, 0, 0);
+    }
+  }
+}
+
+template <typename K_, bool RELU, int ACT, bool HG>
+__global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
+  constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
+  constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
+  constexpr int RING = 2 * TILEB;   // 128 KiB
+  constexpr int TN = 64, TM = 128;
+  constexpr int SLAB = 16 * TN * 2;              // epilogue slab per wave (1 fragment row)
+  constexpr int CST = 1024;                      // column-constant slot per wave and tile parity
+  constexpr int ESTORES = 8 * 16 * TN * 2 / 1024; // 16-B stores per lane per tile
+  // ring | 8 slabs | 8 x 2 const slots = 128 + 16 + 16 KiB
+  __shared__ __attribute__((aligned(1024))) char smem[RING + 8 * SLAB + 16 * CST];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int T = p.tiles_m * p.tiles_n;
+  const int KT = p.K / 64;
+  // Tile order: per-XCD ticket queues (p.tq, KT >= 5: a workgroup that starts late -- its CU
+  // still held by a side-stream kernel -- just takes fewer tiles), else the static walk
+  // wgid, wgid + G, ...  With queues the next tile's ticket is drawn by thread 0 at K step 0
+  // of the current tile (an inline-asm atomic, so hipcc adds no vmcnt(0) for it: it is older
+  // than every load the counted waits target, so they stay correct), read back at step 1
+  // after phase 3's wait has retired it, and published in an LDS word every wave reads at
+  // step 2 -- before the B cursor needs it (step KT - 3).
+  const bool dyn = p.tq != nullptr && KT >= 5;
+  int* const tslot = (int*)(smem + RING);   // wave 0's epilogue slab, word 0 (free outside epilogues)
+  int home = 0, tq_q = 0;                   // thread 0: home queue, queues found empty so far
+  unsigned tk = 0;                          // thread 0: ticket in flight
+  int t_cur;
+  if (dyn) {
+    if (tid == 0) {
+      unsigned xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      home = (int)(xcc & 7);
+      tslot[0] = tq_draw(p.tq, G, T, home, tq_q);
+    }
+    lds_barrier();
+    t_cur = __builtin_amdgcn_readfirstlane(tslot[0]);
+  } else {
+    const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    t_cur = wgid < T ? wgid : -1;
+  }
+  // every workgroup counts itself out; the last one resets the queues for the next launch
+  auto leave = [&]() {
+    if (dyn && tid == 0) {
+      const unsigned d = __hip_atomic_fetch_add(p.tq + TQ_STRIDE * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == (unsigned)G - 1u) {
+        #pragma unroll
+        for (int x = 0; x <= 8; ++x) __hip_atomic_store(p.tq + TQ_STRIDE * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  if (t_cur < 0) {
+    leave();
+    return;
+  }
+  // the tile after t in the static walk (queues: the drawn t_nxt, known from step 2 on)
+  auto static_next = [&](int t) { return t + G < T ? t + G : -1; };
+  int t_nxt = dyn ? -1 : static_next(t_cur);
+
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
+
+  // issue cursors: the next A K tile to stream is global step sa (tile ta, k ka), the next B
+  // K tile step sb (tile tb, k kb); a cursor whose tile is -1 is done.  A cursor is at most one
+  // tile ahead of the tile being computed with queues (two in the static walk at KT = 2), so
+  // it wraps to t_nxt / the static successor.  32-bit element offsets of this lane's rows
+  // (host: M * lda, N * ldb < 2^31).
+  int sa = 0, ta = t_cur, ka = 0, sb = 0, tb = t_cur, kb = 0;
+  int aoff[2][2], boff[2][2];
+  auto a_tile = [&](int t) {
+    int tm, tn;
+    tile_coords(p, t, tm, tn);
+    #pragma unroll
+    for (int h = 0; h < 2; ++h)
+      #pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = tm * 256 + 128 * h + j * 64 + prow;
+        aoff[h][j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
+      }
+  };
+  auto b_tile = [&](int t) {
+    int tm, tn;
+    tile_coords(p, t, tm, tn);
+    #pragma unroll
+    for (int h = 0; h < 2; ++h)
+      #pragma unroll
+      for (int j = 0; j < 2; ++j) boff[h][j] = (tn * 256 + 128 * h + j * 64 + prow) * (int)p.ldb + pchunk * 8;
+  };
+  auto succ = [&](int t) { return dyn ? t_nxt : static_next(t); };
+  auto issueA = [&](int h) {   // A half h of step sa -> buffer sa & 1
+    const uint32_t dst = lds_base + (sa & 1) * TILEB + h * HALF;
+    #pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(p.A + (aoff[h][j] + ka * 64), dst + j * 8192);
+  };
+  auto nextA = [&]() {
+    ++sa;
+    if (++ka == KT) {
+      ka = 0;
+      ta = succ(ta);
+      if (ta >= 0) a_tile(ta);
+    }
+  };
+  auto issueB = [&](int h) {
+    const uint32_t dst = lds_base + (sb & 1) * TILEB + (2 + h) * HALF;
+    #pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(p.B + (boff[h][j] + kb * 64), dst + j * 8192);
+  };
+  auto nextB = [&]() {
+    ++sb;
+    if (++kb == KT) {
+      kb = 0;
+      tb = succ(tb);
+      if (tb >= 0) b_tile(tb);
+    }
+  };
+  f32x4_t acc[8][4];
+  const int frow = lane & 15, fchunk = lane >> 4;
+  uint4 af[2][4], bf[2][2][2];
+  auto readA = [&](int qm, int buf) {
+    const u16* sa_ = (const u16*)(smem + buf * TILEB + wm * HALF);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+        af[ks][fm] = *(const uint4*)(sa_ + lds_off(qm * 64 + fm * 16 + frow, ks * 4 + fchunk));
+  };
+  auto readB = [&](int qn, int buf) {
+    const u16* sb_ = (const u16*)(smem + buf * TILEB + (2 + (wn >> 1)) * HALF);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+        bf[qn][ks][fn] = *(const uint4*)(sb_ + lds_off((wn & 1) * 64 + qn * 32 + fn * 16 + frow, ks * 4 + fchunk));
+  };
+  // FIRST: a tile's first K step -- its ks = 0 MFMAs start from a zero accumulator (no
+  // per-tile clearing of the 128 accumulator registers)
+  auto mma = [&](int qm, int qn, auto first) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fm = 0; fm < 4; ++fm) {
+        uint4 a = af[ks][fm];
+        if constexpr (RELU) a = relu_pk16(a);
+        #pragma unroll
+        for (int fn = 0; fn < 2; ++fn) {
+          f32x4_t& c = acc[qm * 4 + fm][qn * 2 + fn];
+          if constexpr (decltype(first)::value) c = K_::mfma16(bf[qn][ks][fn], a, ks == 0 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : c);
+          else c = K_::mfma16(bf[qn][ks][fn], a, c);
+        }
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void*)p.C, (short)0, (int)p.c_bytes, 0x00020000);
+  char* slab = smem + RING + wave * SLAB;
+  // column constants of tile t -> this wave's const slot `par`: ONE LDS-DMA piece per wave
+  // (lanes 0-15: bias of the wave's 64 columns, 16-31: gamma, 32-63 repeat 0-31), issued
+  // with the tile's loads and retired by the same counted waits (only this wave reads it)
+  auto issue_cst = [&](int t, int par) {
+    int tm, tn;
+    tile_coords(p, t, tm, tn);
+    const int l = lane & 15, n = tn * 256 + wn * TN + 4 * l;
+    const float* src;
+    if ((lane & 16) == 0) src = p.bias ? p.bias + n : (const float*)g_zero_page + 4 * l;
+    else src = HG ? p.gamma + n : (const float*)g_zero_page + 4 * l;
+    glds16(src, __builtin_amdgcn_readfirstlane(lds_addr(smem)) + RING + 8 * SLAB + (wave_u * 2 + par) * CST);
+  };
+
+  // prologue: tile 0's column constants, step 0 (A and B) and step 1's B (KT >= 2)
+  issue_cst(t_cur, 0);
+  a_tile(t_cur);
+  b_tile(t_cur);
+  issueA(0); issueA(1); nextA();
+  issueB(0); issueB(1); nextB();
+  issueB(0); issueB(1); nextB();
+  wait_vmcnt<4>();
+  lds_barrier();
+  // wave rows staggered by one barrier (gemm_8ph_kernel); kept across tiles
+  if (wm == 1) bar();
+  int s = 0;
+  // one K step s (k-th of the i-th tile): the 8-phase schedule of gemm_8ph_kernel with the
+  // issue cursors deciding what streams in
+  auto step = [&](int i, int k, auto first) {
+    const int buf = s & 1;
+    const bool a1 = sa == s + 1 && ta >= 0;   // step s+1's A not issued yet (it was at a boundary)
+    const bool b2 = tb >= 0;                  // sb == s + 2
+    if (dyn && k == 2) t_nxt = __builtin_amdgcn_readfirstlane(tslot[0]);
+    // phase 0: quadrant (0,0)
+    readA(0, buf); readB(0, buf);
+    if (dyn && k == 0 && tid == 0 && tq_q < 8) {
+      const unsigned* q = p.tq + TQ_STRIDE * ((home + tq_q) & 7);
+      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(tk) : "v"(q), "v"(1u) : "memory");
+    }
+    if (a1) issueA(0);
+    bar(); mma(0, 0, first); bar();
+    // phase 1: quadrant (0,1)
+    readB(1, buf);
+    if (a1) { issueA(1); nextA(); }
+    bar(); mma(0, 1, first); bar();
+    // phase 2: quadrant (1,0)
+    readA(1, buf);
+    if (b2) issueB(0);
+    bar(); mma(1, 0, first); bar();
+    // phase 3: step s+1 must have landed before this phase's first barrier; younger than
+    // it: B0 of step s+2 (this step's phase 2) and, in a tile's first step, the previous
+    // tile's epilogue stores (issued after step s+1's loads) and the ticket atomic
+    if (k == 0 && i > 0) {
+      if (b2) wait_vmcnt<ESTORES + 2>(); else wait_vmcnt<ESTORES>();
+    } else {
+      if (b2) wait_vmcnt<2>(); else wait_vmcnt<0>();
+    }
+    if (dyn && k == 1 && tid == 0) {
+      // the wait above retired the ticket (older than this step's loads)
+      asm volatile("" : "+v"(tk));
+      int tn_ = -1;
+      if (tq_q < 8) {
+        tn_ = tq_map(G, T, (home + tq_q) & 7, tk);
+        if (tn_ < 0) {
+          ++tq_q;
+          tn_ = tq_draw(p.tq, G, T, home, tq_q);
+        }
+      }
+      tslot[0] = tn_;   // retired by the lgkmcnt(0) in mma(), before the barrier after it
+    }
+    if (b2) { issueB(1); nextB(); }
+    bar(); mma(1, 1, first);
+    bar();
+    ++s;
+  };
+  for (int i = 0;; ++i) {
+    step(i, 0, std::true_type{});
+    for (int k = 1; k < KT; ++k) step(i, k, std::false_type{});
+    // tile boundary: the next tile's second A K tile goes out before the epilogue's stores
+    // (its buffer's last reads were this step's phases 0 / 2, two barriers back)
+    if (t_nxt >= 0) {
+      if (ta >= 0) { issueA(0); issueA(1); nextA(); }
+      issue_cst(t_nxt, (i + 1) & 1);
+    }
+    int tm, tn;
+    tile_coords(p, t_cur, tm, tn);
+    const float* cst = (const float*)(smem + RING + 8 * SLAB + (wave * 2 + (i & 1)) * CST);
+    epilogue_mfma_buf<K_, ACT, HG>(p, acc, slab, cst, lane, tm * 256 + wm * TM, tn * 256 + wn * TN, crs);
+    if (t_nxt < 0) break;
+    t_cur = t_nxt;
+    if (!dyn) t_nxt = static_next(t_cur);
+  }
+  if (wm == 0) bar();
+  leave();
+}
+
+template <typename K_>
+int launch_p8ph(const GemmP& p0, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = p.N / 256;
+  p.tiles_m = (p.M + 255) / 256;
+  const int T = p.tiles_n * p.tiles_m;
+  const int ea = fast_epi_act(p);
+  if (p.N % 256 || p.K < 128 || !p.c_bytes || p.c_dtype == DP_F32 || ea < 0 || ea >= EPI_ACC) return DP_ERR_ARG;
+  int G = num_cus();
+  if (G > T) G = T;
+  dim3 grid(G);
+#define DP_P8(R_, G_) do { \
+    if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_NONE, G_>), grid, dim3(512), 0, s, p); \
+    else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_RELU, G_>), grid, dim3(512), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_GELU, G_>), grid, dim3(512), 0, s, p); } while (0)
+  // (a gamma-free launch -- fc1 -- skips the multiply by 1 per output)
+  if (p.relu_a) { if (p.gamma) DP_P8(true, true); else DP_P8(true, false); }
+  else { if (p.gamma) DP_P8(false, true); else DP_P8(false, false); }
+#undef DP_P8
   DP_CHECK_LAUNCH();
   return 0;
 }

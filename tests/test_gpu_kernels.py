@@ -623,3 +623,51 @@ def test_infer_epilogue_counts_nonfinite_and_keeps_nan(cuda):
     canon[0, 0, 900, 11] = 1.0
     ops.infer_epilogue(canon, torch.full_like(fov, float("nan")), None, 1536, 1536, depth, fpx, bad)
     assert int(bad) == 1 + 1536 * 1536       # f_px and every depth value
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("case", ["fc1_gelu", "qkv_gamma", "ragged_few_tiles", "k128_many_tiles", "relu_a_n256"])
+def test_persistent_8phase_bit_identical_to_8phase(cuda, dt, case):
+    """The persistent 8-phase engine (DP_TILE_P8PH_256x256: the workgroup's tiles as one stream of
+    K steps, the next tile's loads in flight under each epilogue, column constants by LDS-DMA,
+    counted buffer stores) computes every tile exactly as the 8-phase engine: bit-identical C,
+    incl. ragged last M tiles, K = 128 (a tile boundary every other step) and > 1 tile per
+    workgroup; and both match fp32 torch."""
+    from depth_pro._lib import DP_TILE_P8PH_256x256
+
+    g = torch.Generator().manual_seed(sum(map(ord, case)))
+    M, N, K = {"fc1_gelu": (20195, 4096, 1024), "qkv_gamma": (20195, 3072, 1024),
+               "ragged_few_tiles": (4999, 1536, 512), "k128_many_tiles": (20000, 2048, 128),
+               "relu_a_n256": (9000, 256, 576)}[case]
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    kw = dict(M=M, N=N, K=K, bias=bias)
+    ref = A.float() @ B.float().t() + bias
+    if case in ("fc1_gelu", "ragged_few_tiles"):
+        kw.update(act=DP_ACT_GELU)
+        ref = F.gelu(ref)
+    if case == "qkv_gamma":
+        gamma = torch.rand(N, generator=g).to(cuda) + 0.5
+        kw.update(gamma=gamma)
+        ref = ref * gamma
+    if case == "relu_a_n256":
+        kw.update(relu_a=True)
+        ref = F.relu(A.float()) @ B.float().t() + bias
+    C1 = torch.full((M, N), 7.0, dtype=dt, device=cuda)
+    C2 = C1.clone()
+    C3 = C1.clone()
+    ops.gemm(A, B, C1, tile=DP_TILE_P8PH_256x256, **kw)                    # static tile walk
+    ops.gemm(A, B, C2, tile=DP_TILE_8PH_256x256, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2), (C1.float() - C2.float()).abs().max().item()
+    close(C1, ref, dt, f"p8ph {case}")
+    # with a workspace: per-XCD tile-ticket queues (K >= 320); three launches back to back (the
+    # last workgroup of each resets the queues for the next)
+    ws = ops.gemm_workspace(cuda)
+    for _ in range(3):
+        C3.fill_(7.0)
+        ops.gemm(A, B, C3, tile=DP_TILE_P8PH_256x256, workspace=ws, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(C3, C2), (C3.float() - C2.float()).abs().max().item()
+    assert int(ws[2048:3200].view(torch.int32).abs().sum().item()) == 0, "tile queues not reset"
