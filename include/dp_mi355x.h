@@ -129,7 +129,7 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
        DP_TILE_DEEP5_256x256 = 10, DP_TILE_DEEP_256x128 = 11, DP_TILE_STREAMK_256x256 = 12,
        DP_TILE_BIG_320x256 = 13, DP_TILE_BIG_512x128 = 14, DP_TILE_PBIG_320x256 = 15,
        DP_TILE_PBIG_256x256 = 16, DP_TILE_DUAL_256x128 = 17,
-       DP_TILE_P8PH_256x256 = 18 };
+       DP_TILE_P8PH_256x256 = 18, DP_TILE_8PH_320x256 = 19 };
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 

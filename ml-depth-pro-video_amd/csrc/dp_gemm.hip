@@ -32,6 +32,7 @@ int launch_tile(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s) {
     case DP_TILE_256x64: case DP_TILE_256x32: case DP_TILE_128x128: case DP_TILE_DUAL_256x128:
       return launch_part_small(p, tile, conv, bf16, s);
     case DP_TILE_8PH_256x256: case DP_TILE_P8PH_256x256: return launch_part_8ph(p, tile, conv, bf16, s);
+    case DP_TILE_8PH_320x256: return launch_part_8ph320(p, conv, bf16, s);
     case DP_TILE_BIG_320x256: case DP_TILE_BIG_512x128: return launch_part_big320(p, tile, conv, bf16, s);
     default: return launch_part_big(p, tile, conv, bf16, s);
   }
@@ -192,13 +193,27 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       tile = DP_TILE_PBIG_256x256;
   }
   // the persistent 8-phase engine: dense, N % 256 == 0, K >= 128, the load-free epilogue with a
-  // 16-bit C and bounded buffer stores (A/B: debug 1 << 22 puts the 8-phase launches on it)
-  if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && (dbg & (1 << 22)))) {
+  // 16-bit C and bounded buffer stores -- the planner's 8-phase launches (ViT fc1) run on it
+  // (in-frame A/B, profiles/r03c_p8ph, r03d: 46.67 -> 46.79 / 46.95 fps; debug 1 << 22: off)
+  if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && !(dbg & (1 << 22)))) {
     const bool ok = a->a_mode == DP_A_DENSE && a->N % 256 == 0 && a->K >= 128 && c_bytes && a->c_dtype != DP_F32 &&
                     a->store_mode == DP_STORE_ROWS && !a->R1 && !a->R2 && !a->pos && !a->accumulate &&
                     !a->row_group && !a->head_w && !a->head_corr && !(dbg & (1 << 20));
     if (tile == DP_TILE_P8PH_256x256 && !ok) return DP_ERR_ARG;
     if (ok) tile = DP_TILE_P8PH_256x256;
+  }
+  // the 8-phase 320 x 256 engine: dense, no ReLU prologue, N % 256 == 0, and an epilogue it has
+  // (load-free with a 16-bit C, or the fp32 residual accumulate without activation) -- the
+  // planner's dense 320 x 256 launches (ViT qkv / proj / fc2) run on it (qkv 130.6 -> 115.8,
+  // fc2 149.6 -> 142.0 us, profiles/r03d_8ph320; debug 1 << 15: off)
+  if (tile == DP_TILE_8PH_320x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_BIG_320x256 && !(dbg & (1 << 15)))) {
+    const bool plain = a->a_mode == DP_A_DENSE && !a->relu_a && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
+                       !a->R1 && !a->R2 && !a->pos && !a->row_group && !a->head_w && !a->head_corr &&
+                       !(dbg & (1 << 20));
+    const bool epi_ok = (!a->accumulate && a->c_dtype != DP_F32) ||
+                        (a->accumulate && a->c_dtype == DP_F32 && a->act == DP_ACT_NONE);
+    if (tile == DP_TILE_8PH_320x256 && !(plain && epi_ok)) return DP_ERR_ARG;
+    if (plain && epi_ok) tile = DP_TILE_8PH_320x256;
   }
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
   // the border-corrected composed conv exists in the 512 x 128 conv engine only
@@ -225,8 +240,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   p.dbg = dbg;
   p.c_bytes = c_bytes;
-  // tile-ticket queues of the persistent 8-phase engine (debug 1 << 23: static walk, A/B)
-  p.tq = (ws_ok && !(dbg & (1 << 23))) ? (unsigned*)((char*)a->workspace + TQ_BYTE_OFF) : nullptr;
+  // tile-ticket queues of the persistent 8-phase engine: opt-in (debug 1 << 23); the static walk
+  // measured faster in-frame (44.98 / 44.96 vs 44.63 / 44.56 fps, profiles/r03c_p8ph)
+  p.tq = (ws_ok && (dbg & (1 << 23))) ? (unsigned*)((char*)a->workspace + TQ_BYTE_OFF) : nullptr;
   p.groups = 1;
   p.stagger_wg = 0;
   p.stagger_sleeps = 0;
@@ -249,7 +265,7 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
     case DP_TILE_BIG_320x256: bm = 320; bn = 256; break;
     case DP_TILE_BIG_512x128: bm = 512; bn = 128; break;
     case DP_TILE_DUAL_256x128: bn = 128; break;
-    case DP_TILE_PBIG_320x256: bm = 320; bn = 256; break;
+    case DP_TILE_PBIG_320x256: case DP_TILE_8PH_320x256: bm = 320; bn = 256; break;
     default: bn = 256;
   }
   if (tile_out) *tile_out = tile;

@@ -97,6 +97,7 @@ int num_cus();
 int launch_part_big(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);      // dp_gemm_big.hip
 int launch_part_big320(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);   // dp_gemm_big320.hip
 int launch_part_8ph(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);      // dp_gemm_8ph.hip
+int launch_part_8ph320(const GemmP& p, bool conv, bool bf16, hipStream_t s);             // dp_gemm_8ph320.hip
 int launch_part_pbig(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);     // dp_gemm_pbig.hip
 int launch_part_small(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);    // dp_gemm_small.hip
 int launch_part_sk(const GemmP& p, bool conv, void* ws, bool bf16, hipStream_t s);       // dp_gemm_sk.hip
@@ -544,7 +545,7 @@ __device__ __forceinline__ void epilogue_mfma(const GemmP& p, f32x4_t (&acc)[FM]
                                               int m_base, int n_base) {
   constexpr int CH = TN / 8;            // 16-B chunks per staged row
   constexpr int RPI = 64 / CH;          // rows per read-back instruction
-  static_assert(FM % PF == 0 && (CH == 8 || CH == 4), "tile");
+  static_assert(FM % PF == 0 && (CH == 16 || CH == 8 || CH == 4), "tile");
   const int t = lane & 15, g = lane >> 4;
   float bias[FN][4], gam[FN][4];
   #pragma unroll
@@ -636,6 +637,62 @@ __device__ __forceinline__ void epilogue_acc32(const GemmP& p, f32x4_t (&acc)[FM
     }
     #pragma unroll
     for (int fn = 0; fn < FN; ++fn) cur[fn] = nxt[fn];
+  }
+}
+
+// epilogue_acc32 for wide wave tiles (FN = 8: the 8-phase 320 x 256 engine), where 8 columns'
+// bias / gamma and two rows of C in flight would not fit beside the 160 accumulators: the
+// wave's bias / gamma go through its LDS slab (ds_read per half row), and C is read and
+// written in half rows (4 fragments = 64 columns), the next half row's loads in flight while
+// one is computed.  Same arithmetic in the same order as epilogue_acc32: bit-identical.
+template <int ACT, int FM, int FN>
+__device__ __forceinline__ void epilogue_acc32_wide(const GemmP& p, f32x4_t (&acc)[FM][FN], char* slab, int lane,
+                                                    int m_base, int n_base) {
+  #pragma clang fp contract(off)
+  static_assert(FN == 8, "wide epilogue");
+  constexpr int H = FN / 2;
+  const int t = lane & 15, g = lane >> 4;
+  {
+    // lanes 0-31: bias of columns 4 lane .. +3; lanes 32-63: gamma (1 and 0 when absent)
+    const int c = 4 * (lane & 31), n = n_base + c;
+    f32x4_t v;
+    if (lane < 32) v = (p.bias && n < p.N) ? *(const f32x4_t*)(p.bias + n) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    else v = (p.gamma && n < p.N) ? *(const f32x4_t*)(p.gamma + n) : f32x4_t{1.f, 1.f, 1.f, 1.f};
+    *(f32x4_t*)(slab + (lane < 32 ? 0 : 512) + c * 4) = v;
+  }
+  float* const C = (float*)p.C;
+  f32x4_t cur[H], nxt[H];
+  auto load = [&](int ch, f32x4_t (&c)[H]) __attribute__((always_inline)) {
+    const int fm = ch >> 1, h = ch & 1;
+    const int m = min(m_base + fm * 16 + t, p.M - 1);
+    #pragma unroll
+    for (int f = 0; f < H; ++f)
+      c[f] = *(const f32x4_t*)(C + (long long)m * p.ldc + n_base + (h * H + f) * 16 + 4 * g);
+  };
+  load(0, cur);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slab writes, before any read of them
+  #pragma unroll
+  for (int ch = 0; ch < 2 * FM; ++ch) {
+    if (ch + 1 < 2 * FM) load(ch + 1, nxt);
+    const int fm = ch >> 1, h = ch & 1;
+    const int m = m_base + fm * 16 + t;
+    #pragma unroll
+    for (int f = 0; f < H; ++f) {
+      const int fn = h * H + f;
+      const f32x4_t b = *(const f32x4_t*)(slab + (fn * 16 + 4 * g) * 4);
+      const f32x4_t q = *(const f32x4_t*)(slab + 512 + (fn * 16 + 4 * g) * 4);
+      f32x4_t x;
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[fm][fn][r] + b[r];
+        if constexpr (ACT == DP_ACT_RELU) v = fmaxf(v, 0.f);
+        else if constexpr (ACT == DP_ACT_GELU) v = gelu_erf(v);
+        x[r] = v * q[r] + cur[f][r];
+      }
+      if (m < p.M) *(f32x4_t*)(C + (long long)m * p.ldc + n_base + fn * 16 + 4 * g) = x;
+    }
+    #pragma unroll
+    for (int f = 0; f < H; ++f) cur[f] = nxt[f];
   }
 }
 
@@ -1927,6 +1984,174 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
   if (p.relu_a) { if (p.gamma) DP_P8(true, true); else DP_P8(true, false); }
   else { if (p.gamma) DP_P8(false, true); else DP_P8(false, false); }
 #undef DP_P8
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+
+// ======================================================= 8-phase 320x256 engine
+// The 8-phase schedule (gemm_8ph_kernel) on the 320 x 256 tile that gives the ViT's M = 20195
+// exactly 64 row tiles (proj / fc2: ONE round of 256 workgroups; qkv: 3).  8 waves as 4 (M) x
+// 2 (N), wave tile 80 x 128 (acc 5 x 8 fragments = 160 VGPRs).  A K step (BK 64) is 4 phases,
+// one per 32-column quarter of the wave's 128 columns: {ds_reads, LDS-DMA pieces, counted
+// vmcnt, s_barrier, 20 MFMAs at raised priority, s_barrier}; phase 0 also reads the wave's 10
+// A fragments (kept for the step).  The two wave groups (waves 0-3 / 4-7: one of each per
+// SIMD) run staggered by one barrier, so one wave of a SIMD issues MFMAs while the other reads.
+// LDS: 2 K-tile buffers of A (320 x 128 B) + B (256 x 128 B) = 144 KiB.
+// Streaming, per step s (9 pieces of 1 KiB per wave): B quarter q of step s+1 in phase q (its
+// buffer's quarter was last read 4 phases earlier), A of step s+2 in phases 2 / 3 (3 + 2
+// pieces; the buffer's A was read in phase 0, two barriers back).  Every phase waits (counted)
+// for what the NEXT phase reads -- B quarter q+1 of this step, or A and B quarter 0 of step
+// s+1 in phase 3 -- so each piece has 4+ phases to land and the count is 8 in steady state.
+// Dense A only; epilogues: the load-free MFMA-layout one (EACT = DP_ACT_*; 16-bit C) or the
+// fp32 residual-accumulate one (EACT = EPI_ACC + act).
+template <typename K_, int EACT>
+__global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
+  constexpr int BM = 320;
+  constexpr int A_BYTES = BM * 128, B_BYTES = 256 * 128, BUF = A_BYTES + B_BYTES;
+  constexpr int FM = 5, FN = 8, TM = 80, TN = 128;
+  constexpr int RING = 2 * BUF;                                   // 144 KiB
+  constexpr int PF = 1, SLAB = PF * 16 * TN * 2;                  // epilogue_mfma slab per wave
+  constexpr int SMEM = RING > 8 * SLAB ? RING : 8 * SLAB;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave & 3, wn = wave >> 2;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  int tile_m, tile_n;
+  tile_coords(p, wgid, tile_m, tile_n);
+  const int m0 = tile_m * BM, n0 = tile_n * 256;
+
+  // LDS-DMA pieces: 8 rows x 128 B per wave, the 16-B chunk swizzled on the source address
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  int aoff[5];
+  #pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int m = m0 + j * 64 + wave * 8 + (lane >> 3);
+    aoff[j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
+  }
+  // B quarter q = output columns {q*32 .. +31} u {128 + q*32 .. +31}: waves 0-3 / 4-7 take 8 rows each
+  const int brow0 = wave_u < 4 ? wave_u * 8 : 128 + (wave_u - 4) * 8;   // + q * 32
+  const int boff = (n0 + brow0 + (lane >> 3)) * (int)p.ldb + pchunk * 8;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  auto issueA = [&](int j, int t) {
+    glds16(p.A + (aoff[j] + t * 64), lds0 + (t & 1) * BUF + j * 8192 + wave_u * 1024);
+  };
+  auto issueB = [&](int q, int t) {
+    glds16(p.B + (boff + q * 32 * (int)p.ldb + t * 64), lds0 + (t & 1) * BUF + A_BYTES + (brow0 + q * 32) * 128);
+  };
+
+  f32x4_t acc[FM][FN];
+  #pragma unroll
+  for (int i = 0; i < FM; ++i)
+    #pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int frow = lane & 15, fchunk = lane >> 4;
+  uint4 af[2][FM], bf[2][2];
+  auto readA = [&](int buf) {
+    const u16* sa = (const u16*)(smem + buf * BUF);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+        af[ks][fm] = *(const uint4*)(sa + lds_off(wm * TM + fm * 16 + frow, ks * 4 + fchunk));
+  };
+  auto readB = [&](int q, int buf) {
+    const u16* sb = (const u16*)(smem + buf * BUF + A_BYTES);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int f = 0; f < 2; ++f)
+        bf[ks][f] = *(const uint4*)(sb + lds_off(wn * TN + q * 32 + f * 16 + frow, ks * 4 + fchunk));
+  };
+  auto mma = [&](int q) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+        #pragma unroll
+        for (int f = 0; f < 2; ++f) acc[fm][2 * q + f] = K_::mfma16(bf[ks][f], af[ks][fm], acc[fm][2 * q + f]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
+
+  const int KT = p.K / 64;
+  // prologue = "step -1" in the steady-state issue order: A(0); Bq0..3(0) with A(1) after Bq2 / Bq3
+  #pragma unroll
+  for (int j = 0; j < 5; ++j) issueA(j, 0);
+  issueB(0, 0);
+  issueB(1, 0);
+  issueB(2, 0);
+  if (KT > 1) { issueA(0, 1); issueA(1, 1); issueA(2, 1); }
+  issueB(3, 0);
+  if (KT > 1) { issueA(3, 1); issueA(4, 1); }
+  // A(0) and Bq0(0) landed: younger are Bq1..3(0) and A(1)
+  if (KT > 1) wait_vmcnt<8>(); else wait_vmcnt<3>();
+  lds_barrier();
+  if (wave >= 4) bar();
+  for (int s = 0; s < KT; ++s) {
+    const int buf = s & 1;
+    const bool a1 = s + 1 < KT, a2 = s + 2 < KT;
+    // phase 0: A fragments + B quarter 0; retire Bq1(s) (younger: 2 + 6 a1)
+    readA(buf); readB(0, buf);
+    if (a1) issueB(0, s + 1);
+    if (a1) wait_vmcnt<8>(); else wait_vmcnt<2>();
+    bar(); mma(0); bar();
+    // phase 1: retire Bq2(s) (younger: 1 + 7 a1)
+    readB(1, buf);
+    if (a1) issueB(1, s + 1);
+    if (a1) wait_vmcnt<8>(); else wait_vmcnt<1>();
+    bar(); mma(1); bar();
+    // phase 2: A(s+2) pieces 0-2 into this step's buffer; retire Bq3(s) (younger: 5 a1 + 3 a2)
+    readB(2, buf);
+    if (a1) issueB(2, s + 1);
+    if (a2) { issueA(0, s + 2); issueA(1, s + 2); issueA(2, s + 2); }
+    if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<5>(); else wait_vmcnt<0>();
+    bar(); mma(2); bar();
+    // phase 3: retire A(s+1) and Bq0(s+1) (younger: 3 + 5 a2)
+    readB(3, buf);
+    if (a1) issueB(3, s + 1);
+    if (a2) { issueA(3, s + 2); issueA(4, s + 2); }
+    if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<3>();
+    bar(); mma(3); bar();
+  }
+  if (wave < 4) bar();
+  if (p.dbg & 1) {   // ablation (tools/gemm_bench.py --ablate): no epilogue
+    #pragma unroll
+    for (int i = 0; i < FM; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(acc[i][j][0]), "v"(acc[i][j][1]), "v"(acc[i][j][2]), "v"(acc[i][j][3]));
+    return;
+  }
+  lds_barrier();   // the ring is free once every wave has left the K loop
+  if constexpr (EACT >= EPI_ACC)
+    epilogue_acc32_wide<EACT - EPI_ACC, FM, FN>(p, acc, smem + wave * SLAB, lane, m0 + wm * TM, n0 + wn * TN);
+  else
+    epilogue_mfma<K_, EACT, FM, FN, TN, PF>(p, acc, smem + wave * SLAB, lane, m0 + wm * TM, n0 + wn * TN);
+}
+
+template <typename K_>
+int launch_8ph320(const GemmP& p0, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = p.N / 256;
+  p.tiles_m = (p.M + 319) / 320;
+  const int ea = fast_epi_act(p);
+  if (p.N % 256 || ea < 0 || p.relu_a) return DP_ERR_ARG;
+  dim3 grid(p.tiles_n * p.tiles_m);
+  switch (ea) {
+    case DP_ACT_NONE: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, DP_ACT_NONE>), grid, dim3(512), 0, s, p); break;
+    case DP_ACT_RELU: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, DP_ACT_RELU>), grid, dim3(512), 0, s, p); break;
+    case DP_ACT_GELU: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, DP_ACT_GELU>), grid, dim3(512), 0, s, p); break;
+    case EPI_ACC + DP_ACT_NONE: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE>), grid, dim3(512), 0, s, p); break;
+    default: return DP_ERR_ARG;
+  }
   DP_CHECK_LAUNCH();
   return 0;
 }

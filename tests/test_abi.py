@@ -76,9 +76,13 @@ def test_gemm_plan_tile_choice():
         return rc, t.value, g.value
 
     # ViT-L patch encoder (M = 35 x 577 = 20195 = 64 tiles of 320 rows)
-    assert plan(20195, 3072, 1024)[1:] == (_lib.DP_TILE_BIG_320x256, 64 * 12)
-    assert plan(20195, 1024, 1024)[1:] == (_lib.DP_TILE_BIG_320x256, 64 * 4)     # one round on 256 CUs
-    assert plan(20195, 4096, 1024)[1:] == (_lib.DP_TILE_8PH_256x256, 79 * 16)
+    # qkv / proj: the 8-phase 320 x 256 engine; fc1: the persistent 8-phase engine (one workgroup per CU)
+    assert plan(20195, 3072, 1024)[1:] == (_lib.DP_TILE_8PH_320x256, 64 * 12)
+    assert plan(20195, 1024, 1024)[1:] == (_lib.DP_TILE_8PH_320x256, 64 * 4)     # one round on 256 CUs
+    assert plan(20195, 4096, 1024)[1:] == (_lib.DP_TILE_P8PH_256x256, 256)
+    # the previous engines stay reachable (A/B switches in the planner, explicit tile hints)
+    assert plan(20195, 4096, 1024, tile=_lib.DP_TILE_8PH_256x256)[1:] == (_lib.DP_TILE_8PH_256x256, 79 * 16)
+    assert plan(20195, 1024, 1024, tile=_lib.DP_TILE_BIG_320x256)[1:] == (_lib.DP_TILE_BIG_320x256, 64 * 4)
     assert plan(577, 3072, 1024)[1:] == (_lib.DP_TILE_BIG_256x128, 3 * 24)       # side encoders
     assert plan(768 * 768, 128, 2304)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)     # head.0 conv (N = 128)
     # stream-K is opt-in and needs a workspace

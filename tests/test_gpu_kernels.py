@@ -671,3 +671,45 @@ def test_persistent_8phase_bit_identical_to_8phase(cuda, dt, case):
         torch.cuda.synchronize()
         assert torch.equal(C3, C2), (C3.float() - C2.float()).abs().max().item()
     assert int(ws[2048:3200].view(torch.int32).abs().sum().item()) == 0, "tile queues not reset"
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("case", ["qkv_gamma", "proj_acc", "fc2_acc", "ragged_k192", "k64", "k128_gelu"])
+def test_8phase_320_bit_identical_to_320(cuda, dt, case):
+    """The 8-phase 320 x 256 engine (DP_TILE_8PH_320x256: 4 x 2 waves, one 32-column quarter per
+    phase, counted waits every phase) computes every tile exactly as the 320 x 256 big engine:
+    bit-identical C for the load-free (bias / gamma / GELU, 16-bit C) and the fp32 residual
+    accumulate epilogues, incl. a ragged last row tile and K = 64 / 128 / 192 (the loop's
+    tail issue counts); both match fp32 torch."""
+    from depth_pro._lib import DP_TILE_8PH_320x256
+
+    g = torch.Generator().manual_seed(sum(map(ord, case)) + 3)
+    M, N, K = {"qkv_gamma": (20195, 3072, 1024), "proj_acc": (20195, 1024, 1024), "fc2_acc": (20195, 1024, 4096),
+               "ragged_k192": (1000, 512, 192), "k64": (700, 256, 64), "k128_gelu": (3001, 768, 128)}[case]
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    kw = dict(M=M, N=N, K=K, bias=bias)
+    ref = A.float() @ B.float().t() + bias
+    if case in ("qkv_gamma", "proj_acc", "fc2_acc"):
+        gamma = torch.rand(N, generator=g).to(cuda) + 0.5
+        kw.update(gamma=gamma)
+        ref = ref * gamma
+    if case == "k128_gelu":
+        kw.update(act=DP_ACT_GELU)
+        ref = F.gelu(ref)
+    if case.endswith("_acc"):
+        kw.update(accumulate=True)
+        X = torch.randn(M, N, generator=g).to(cuda)
+        C1, C2 = X.clone(), X.clone()
+        ref = ref + X
+        cdt = torch.float32 if dt == torch.float16 else dt
+    else:
+        C1 = torch.full((M, N), 7.0, dtype=dt, device=cuda)
+        C2 = C1.clone()
+        cdt = dt
+    ops.gemm(A, B, C1, tile=DP_TILE_8PH_320x256, **kw)
+    ops.gemm(A, B, C2, tile=DP_TILE_BIG_320x256, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2), (C1.float() - C2.float()).abs().max().item()
+    close(C1, ref, cdt, f"8ph320 {case}")
