@@ -45,6 +45,14 @@ for S in $STEPS; do
         > $OUT/gemm_sq4096.txt 2>&1
       timeout -k 10 300 python -u tools/gemm_bench.py --tile big320x256,8ph256x256 --only + --ablate \
         > $OUT/gemm_res.txt 2>&1 ;;
+    fc1)
+      # fc1 on the three engines that can run it, same box
+      timeout -k 10 300 python -u tools/gemm_bench.py --tile 8ph256x256,p8ph256x256,8ph320x256 --only fc1 --ablate \
+        > $OUT/gemm_fc1_engines.txt 2>&1 ;;
+    side)
+      # side-encoder cost by ablation (DP_ABLATE=side: image / FOV encoders skipped) vs the full frame
+      DP_ABLATE=side timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $OUT/bench_noside.json 2> $OUT/bench_noside.err
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $OUT/bench_side.json 2> $OUT/bench_side.err ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
   echo "step $S ok"
