@@ -1707,7 +1707,7 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
   }
 }
 
-template <typename K_, bool RELU, int ACT, bool HG>
+template <typename K_, bool CONV, bool RELU, int ACT, bool HG>
 __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
   constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
@@ -1780,7 +1780,11 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   // it wraps to t_nxt / the static successor.  32-bit element offsets of this lane's rows
   // (host: M * lda, N * ldb < 2^31).
   int sa = 0, ta = t_cur, ka = 0, sb = 0, tb = t_cur, kb = 0;
+  // (implicit conv: the A cursor keeps each row's top-left input tap instead of an offset, in
+  // two registers: the tap's pixel index and its (y, x) as two signed 16-bit halves; a row
+  // past M gets y = -16384, out of bounds for every tap)
   int aoff[2][2], boff[2][2];
+  int acr_pix[2][2], acr_yx[2][2];
   auto a_tile = [&](int t) {
     int tm, tn;
     tile_coords(p, t, tm, tn);
@@ -1789,7 +1793,14 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
       #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int m = tm * 256 + 128 * h + j * 64 + prow;
-        aoff[h][j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
+        if constexpr (CONV) {
+          const ConvRow r = conv_row(p, m);
+          const int iy = m < p.M ? r.iy : -16384;
+          acr_pix[h][j] = r.pix + iy * p.in_w + r.ix;
+          acr_yx[h][j] = (int)(((unsigned)iy << 16) | ((unsigned)r.ix & 0xFFFFu));
+        } else {
+          aoff[h][j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
+        }
       }
   };
   auto b_tile = [&](int t) {
@@ -1803,8 +1814,20 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   auto succ = [&](int t) { return dyn ? t_nxt : static_next(t); };
   auto issueA = [&](int h) {   // A half h of step sa -> buffer sa & 1
     const uint32_t dst = lds_base + (sa & 1) * TILEB + h * HALF;
-    #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(p.A + (aoff[h][j] + ka * 64), dst + j * 8192);
+    if constexpr (CONV) {
+      int ky, kx, ci;
+      conv_tap(p, ka * 64, ky, kx, ci);
+      #pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int iy = (acr_yx[h][j] >> 16) + ky, ix = ((int)((unsigned)acr_yx[h][j] << 16) >> 16) + kx;
+        const bool inb = (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
+        const u16* src = p.A + ((long long)(acr_pix[h][j] + ky * p.in_w + kx) * p.in_c + ci + pchunk * 8);
+        glds16(inb ? (const void*)src : (const void*)g_zero_page, dst + j * 8192);
+      }
+    } else {
+      #pragma unroll
+      for (int j = 0; j < 2; ++j) glds16(p.A + (aoff[h][j] + ka * 64), dst + j * 8192);
+    }
   };
   auto nextA = [&]() {
     ++sa;
@@ -1966,7 +1989,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
 }
 
 template <typename K_>
-int launch_p8ph(const GemmP& p0, hipStream_t s) {
+int launch_p8ph(const GemmP& p0, bool conv, hipStream_t s) {
   GemmP p = p0;
   p.tiles_n = p.N / 256;
   p.tiles_m = (p.M + 255) / 256;
@@ -1976,13 +1999,18 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
   int G = num_cus();
   if (G > T) G = T;
   dim3 grid(G);
-#define DP_P8(R_, G_) do { \
-    if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_NONE, G_>), grid, dim3(512), 0, s, p); \
-    else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_RELU, G_>), grid, dim3(512), 0, s, p); \
-    else hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_GELU, G_>), grid, dim3(512), 0, s, p); } while (0)
-  // (a gamma-free launch -- fc1 -- skips the multiply by 1 per output)
-  if (p.relu_a) { if (p.gamma) DP_P8(true, true); else DP_P8(true, false); }
-  else { if (p.gamma) DP_P8(false, true); else DP_P8(false, false); }
+#define DP_P8(C_, R_, G_) do { \
+    if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, C_, R_, DP_ACT_NONE, G_>), grid, dim3(512), 0, s, p); \
+    else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, C_, R_, DP_ACT_RELU, G_>), grid, dim3(512), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_p8ph_kernel<K_, C_, R_, DP_ACT_GELU, G_>), grid, dim3(512), 0, s, p); } while (0)
+  // (a gamma-free launch -- fc1 -- skips the multiply by 1 per output; implicit convs: the decoder's
+  // ResidualBlock first convs, ReLU on load + bias + ReLU, no gamma)
+  if (conv) {
+    if (p.gamma) return DP_ERR_ARG;
+    if (p.relu_a) DP_P8(true, true, false);
+    else DP_P8(true, false, false);
+  } else if (p.relu_a) { if (p.gamma) DP_P8(false, true, true); else DP_P8(false, true, false); }
+  else { if (p.gamma) DP_P8(false, false, true); else DP_P8(false, false, false); }
 #undef DP_P8
   DP_CHECK_LAUNCH();
   return 0;
