@@ -195,10 +195,10 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // the persistent 8-phase engine: dense, N % 256 == 0, K >= 128, the load-free epilogue with a
   // 16-bit C and bounded buffer stores -- the planner's 8-phase launches (ViT fc1) run on it
   // (in-frame A/B, profiles/r03c_p8ph, r03d: 46.67 -> 46.79 / 46.95 fps; debug 1 << 22: off)
-  if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && !(dbg & (1 << 22))) ||
-      (a->tile == DP_TILE_AUTO && tile == DP_TILE_PBIG_256x256 && a->a_mode == DP_A_CONV && (dbg & 4096))) {
-    // (implicit convs -- the decoder's 768^2 ResidualBlock first convs: A/B, debug 4096)
-    const bool ok = (a->a_mode == DP_A_DENSE || !a->gamma) && a->N % 256 == 0 && a->K >= 128 && c_bytes && a->c_dtype != DP_F32 &&
+  // (measured and rejected: an implicit-conv A loader for the 768^2 ResidualBlock convs, 675 vs
+  // 666 us on the persistent big engine, profiles/r03g_conv768_p8ph.txt)
+  if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && !(dbg & (1 << 22)))) {
+    const bool ok = a->a_mode == DP_A_DENSE && a->N % 256 == 0 && a->K >= 128 && c_bytes && a->c_dtype != DP_F32 &&
                     a->store_mode == DP_STORE_ROWS && !a->R1 && !a->R2 && !a->pos && !a->accumulate &&
                     !a->row_group && !a->head_w && !a->head_corr && !(dbg & (1 << 20));
     if (tile == DP_TILE_P8PH_256x256 && !ok) return DP_ERR_ARG;
@@ -242,9 +242,6 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   p.dbg = dbg;
   p.c_bytes = c_bytes;
-  // tile-ticket queues of the persistent 8-phase engine: opt-in (debug 1 << 23); the static walk
-  // measured faster in-frame (44.98 / 44.96 vs 44.63 / 44.56 fps, profiles/r03c_p8ph)
-  p.tq = (ws_ok && (dbg & (1 << 23))) ? (unsigned*)((char*)a->workspace + TQ_BYTE_OFF) : nullptr;
   p.groups = 1;
   p.stagger_wg = 0;
   p.stagger_sleeps = 0;

@@ -70,7 +70,6 @@ struct GemmP {
   int stagger_wg, stagger_sleeps;   // 2-workgroup-per-CU engine: start stagger (debug 1 << 21)
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
   unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
-  unsigned* tq;      // persistent 8-phase engine: tile-ticket queues in the workspace (NULL: static walk)
   // dp_gemm_grouped: `groups` problems of one shape in one launch (workgroup range g * tiles_m *
   // tiles_n ... covers problem g, whose operand pointers are grp[g]); 1 otherwise
   int groups;
@@ -1631,36 +1630,12 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
 // ESTORES buffer stores per lane (every lane stores; rows past M / columns past N get an
 // out-of-range offset, dropped by the hardware), so the count is a compile-time constant.
 // The epilogue is the load-free MFMA-layout one (bias, activation, gamma; 16-bit C) staged
-// through a 4 KiB slab per wave beside the 128 KiB ring (160 KiB of LDS in all), so no LDS
-// the ring uses is touched.  Dense A only (the ViT's fc1 / qkv).  Requires K >= 128.
+// through a 2 KiB slab per wave beside the 128 KiB ring (+ 2 x 1 KiB column-constant slots
+// per wave: 160 KiB of LDS in all), so no LDS the ring uses is touched.  Dense A only (the ViT's fc1 / qkv).  Requires K >= 128.
 // The wave's column constants (bias / gamma of its 64 columns) come from its LDS const slot
 // (filled by LDS-DMA with the tile's loads), so the epilogue issues no global load: hipcc
 // would put a vmcnt(0) in front of one -- a wait for every LDS-DMA in flight, i.e. the next
 // tile's first K steps.
-// Per-XCD tile-ticket queues of the persistent 8-phase engine (workspace bytes [2048, 3200):
-// 8 queue counters + an exit counter, 128 B apart).  Queue x hands out, round by round, the
-// tile positions [x*G/8, (x+1)*G/8) of each round of G tiles -- the XCD-contiguous placement
-// of the static walk -- and a workgroup whose own queue is empty takes from the next XCD's.
-// The last workgroup to finish resets the counters (graph-replay safe, no memset).
-constexpr int TQ_BYTE_OFF = 2048;
-constexpr int TQ_STRIDE = 32;   // uint32 words between counters
-__device__ __forceinline__ int tq_map(int G, int T, int x, unsigned k) {
-  const int c0 = x * G / 8, len = (x + 1) * G / 8 - c0;
-  if (len <= 0) return -1;
-  const long long t = (long long)(k / (unsigned)len) * G + c0 + (int)(k % (unsigned)len);
-  return t < T ? (int)t : -1;
-}
-// thread 0 only: tickets from queue home+q, home+q+1, ... until a valid tile or all 8 are empty
-__device__ __forceinline__ int tq_draw(unsigned* tq, int G, int T, int home, int& q) {
-  for (; q < 8; ++q) {
-    const int x = (home + q) & 7;
-    const unsigned k = __hip_atomic_fetch_add(tq + TQ_STRIDE * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int t = tq_map(G, T, x, k);
-    if (t >= 0) return t;
-  }
-  return -1;
-}
-
 template <typename K_, int ACT, bool HG>
 __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)[8][4], char* slab,
                                                   const float* cst, int lane, int m_base, int n_base,
@@ -1707,7 +1682,7 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
   }
 }
 
-template <typename K_, bool CONV, bool RELU, int ACT, bool HG>
+template <typename K_, bool RELU, int ACT, bool HG>
 __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
   constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
@@ -1726,65 +1701,25 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   const int G = gridDim.x, bid = blockIdx.x;
   const int T = p.tiles_m * p.tiles_n;
   const int KT = p.K / 64;
-  // Tile order: per-XCD ticket queues (p.tq, KT >= 5: a workgroup that starts late -- its CU
-  // still held by a side-stream kernel -- just takes fewer tiles), else the static walk
-  // wgid, wgid + G, ...  With queues the next tile's ticket is drawn by thread 0 at K step 0
-  // of the current tile (an inline-asm atomic, so hipcc adds no vmcnt(0) for it: it is older
-  // than every load the counted waits target, so they stay correct), read back at step 1
-  // after phase 3's wait has retired it, and published in an LDS word every wave reads at
-  // step 2 -- before the B cursor needs it (step KT - 3).
-  const bool dyn = p.tq != nullptr && KT >= 5;
-  int* const tslot = (int*)(smem + RING);   // wave 0's epilogue slab, word 0 (free outside epilogues)
-  int home = 0, tq_q = 0;                   // thread 0: home queue, queues found empty so far
-  unsigned tk = 0;                          // thread 0: ticket in flight
-  int t_cur;
-  if (dyn) {
-    if (tid == 0) {
-      unsigned xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      home = (int)(xcc & 7);
-      tslot[0] = tq_draw(p.tq, G, T, home, tq_q);
-    }
-    lds_barrier();
-    t_cur = __builtin_amdgcn_readfirstlane(tslot[0]);
-  } else {
-    const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    t_cur = wgid < T ? wgid : -1;
-  }
-  // every workgroup counts itself out; the last one resets the queues for the next launch
-  auto leave = [&]() {
-    if (dyn && tid == 0) {
-      const unsigned d = __hip_atomic_fetch_add(p.tq + TQ_STRIDE * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == (unsigned)G - 1u) {
-        #pragma unroll
-        for (int x = 0; x <= 8; ++x) __hip_atomic_store(p.tq + TQ_STRIDE * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  };
-  if (t_cur < 0) {
-    leave();
-    return;
-  }
-  // the tile after t in the static walk (queues: the drawn t_nxt, known from step 2 on)
-  auto static_next = [&](int t) { return t + G < T ? t + G : -1; };
-  int t_nxt = dyn ? -1 : static_next(t_cur);
+  // tile order: the static walk wgid, wgid + G, ... (XCD-contiguous, as the data-parallel
+  // launch's rounds).  Measured and rejected: per-XCD tile-ticket queues (a workgroup that
+  // starts late takes fewer tiles), 44.63 / 44.56 vs 44.98 / 44.96 fps (profiles/r03c_p8ph/).
+  const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  if (wgid >= T) return;
+  auto next_tile = [&](int t) { return t + G < T ? t + G : -1; };
+  int t_cur = wgid, t_nxt = next_tile(t_cur);
 
   const int prow = wave * 8 + (lane >> 3);
   const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave_u * 1024;
 
   // issue cursors: the next A K tile to stream is global step sa (tile ta, k ka), the next B
-  // K tile step sb (tile tb, k kb); a cursor whose tile is -1 is done.  A cursor is at most one
-  // tile ahead of the tile being computed with queues (two in the static walk at KT = 2), so
-  // it wraps to t_nxt / the static successor.  32-bit element offsets of this lane's rows
-  // (host: M * lda, N * ldb < 2^31).
+  // K tile step sb (tile tb, k kb); a cursor whose tile is -1 is done (it wraps to its tile's
+  // successor in the walk: up to two tiles ahead of the one computed at KT = 2).  32-bit
+  // element offsets of this lane's rows (host: M * lda, N * ldb < 2^31).
   int sa = 0, ta = t_cur, ka = 0, sb = 0, tb = t_cur, kb = 0;
-  // (implicit conv: the A cursor keeps each row's top-left input tap instead of an offset, in
-  // two registers: the tap's pixel index and its (y, x) as two signed 16-bit halves; a row
-  // past M gets y = -16384, out of bounds for every tap)
   int aoff[2][2], boff[2][2];
-  int acr_pix[2][2], acr_yx[2][2];
   auto a_tile = [&](int t) {
     int tm, tn;
     tile_coords(p, t, tm, tn);
@@ -1793,14 +1728,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
       #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int m = tm * 256 + 128 * h + j * 64 + prow;
-        if constexpr (CONV) {
-          const ConvRow r = conv_row(p, m);
-          const int iy = m < p.M ? r.iy : -16384;
-          acr_pix[h][j] = r.pix + iy * p.in_w + r.ix;
-          acr_yx[h][j] = (int)(((unsigned)iy << 16) | ((unsigned)r.ix & 0xFFFFu));
-        } else {
-          aoff[h][j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
-        }
+        aoff[h][j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
       }
   };
   auto b_tile = [&](int t) {
@@ -1811,29 +1739,16 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
       #pragma unroll
       for (int j = 0; j < 2; ++j) boff[h][j] = (tn * 256 + 128 * h + j * 64 + prow) * (int)p.ldb + pchunk * 8;
   };
-  auto succ = [&](int t) { return dyn ? t_nxt : static_next(t); };
   auto issueA = [&](int h) {   // A half h of step sa -> buffer sa & 1
     const uint32_t dst = lds_base + (sa & 1) * TILEB + h * HALF;
-    if constexpr (CONV) {
-      int ky, kx, ci;
-      conv_tap(p, ka * 64, ky, kx, ci);
-      #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int iy = (acr_yx[h][j] >> 16) + ky, ix = ((int)((unsigned)acr_yx[h][j] << 16) >> 16) + kx;
-        const bool inb = (unsigned)iy < (unsigned)p.in_h && (unsigned)ix < (unsigned)p.in_w;
-        const u16* src = p.A + ((long long)(acr_pix[h][j] + ky * p.in_w + kx) * p.in_c + ci + pchunk * 8);
-        glds16(inb ? (const void*)src : (const void*)g_zero_page, dst + j * 8192);
-      }
-    } else {
-      #pragma unroll
-      for (int j = 0; j < 2; ++j) glds16(p.A + (aoff[h][j] + ka * 64), dst + j * 8192);
-    }
+    #pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(p.A + (aoff[h][j] + ka * 64), dst + j * 8192);
   };
   auto nextA = [&]() {
     ++sa;
     if (++ka == KT) {
       ka = 0;
-      ta = succ(ta);
+      ta = next_tile(ta);
       if (ta >= 0) a_tile(ta);
     }
   };
@@ -1846,7 +1761,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     ++sb;
     if (++kb == KT) {
       kb = 0;
-      tb = succ(tb);
+      tb = next_tile(tb);
       if (tb >= 0) b_tile(tb);
     }
   };
@@ -1924,13 +1839,8 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     const int buf = s & 1;
     const bool a1 = sa == s + 1 && ta >= 0;   // step s+1's A not issued yet (it was at a boundary)
     const bool b2 = tb >= 0;                  // sb == s + 2
-    if (dyn && k == 2) t_nxt = __builtin_amdgcn_readfirstlane(tslot[0]);
     // phase 0: quadrant (0,0)
     readA(0, buf); readB(0, buf);
-    if (dyn && k == 0 && tid == 0 && tq_q < 8) {
-      const unsigned* q = p.tq + TQ_STRIDE * ((home + tq_q) & 7);
-      asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(tk) : "v"(q), "v"(1u) : "memory");
-    }
     if (a1) issueA(0);
     bar(); mma(0, 0, first); bar();
     // phase 1: quadrant (0,1)
@@ -1943,24 +1853,11 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     bar(); mma(1, 0, first); bar();
     // phase 3: step s+1 must have landed before this phase's first barrier; younger than
     // it: B0 of step s+2 (this step's phase 2) and, in a tile's first step, the previous
-    // tile's epilogue stores (issued after step s+1's loads) and the ticket atomic
+    // tile's epilogue stores (issued after step s+1's loads)
     if (k == 0 && i > 0) {
       if (b2) wait_vmcnt<ESTORES + 2>(); else wait_vmcnt<ESTORES>();
     } else {
       if (b2) wait_vmcnt<2>(); else wait_vmcnt<0>();
-    }
-    if (dyn && k == 1 && tid == 0) {
-      // the wait above retired the ticket (older than this step's loads)
-      asm volatile("" : "+v"(tk));
-      int tn_ = -1;
-      if (tq_q < 8) {
-        tn_ = tq_map(G, T, (home + tq_q) & 7, tk);
-        if (tn_ < 0) {
-          ++tq_q;
-          tn_ = tq_draw(p.tq, G, T, home, tq_q);
-        }
-      }
-      tslot[0] = tn_;   // retired by the lgkmcnt(0) in mma(), before the barrier after it
     }
     if (b2) { issueB(1); nextB(); }
     bar(); mma(1, 1, first);
@@ -1982,14 +1879,13 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     epilogue_mfma_buf<K_, ACT, HG>(p, acc, slab, cst, lane, tm * 256 + wm * TM, tn * 256 + wn * TN, crs);
     if (t_nxt < 0) break;
     t_cur = t_nxt;
-    if (!dyn) t_nxt = static_next(t_cur);
+    t_nxt = next_tile(t_cur);
   }
   if (wm == 0) bar();
-  leave();
 }
 
 template <typename K_>
-int launch_p8ph(const GemmP& p0, bool conv, hipStream_t s) {
+int launch_p8ph(const GemmP& p0, hipStream_t s) {
   GemmP p = p0;
   p.tiles_n = p.N / 256;
   p.tiles_m = (p.M + 255) / 256;
@@ -1999,18 +1895,13 @@ int launch_p8ph(const GemmP& p0, bool conv, hipStream_t s) {
   int G = num_cus();
   if (G > T) G = T;
   dim3 grid(G);
-#define DP_P8(C_, R_, G_) do { \
-    if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, C_, R_, DP_ACT_NONE, G_>), grid, dim3(512), 0, s, p); \
-    else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, C_, R_, DP_ACT_RELU, G_>), grid, dim3(512), 0, s, p); \
-    else hipLaunchKernelGGL((gemm_p8ph_kernel<K_, C_, R_, DP_ACT_GELU, G_>), grid, dim3(512), 0, s, p); } while (0)
-  // (a gamma-free launch -- fc1 -- skips the multiply by 1 per output; implicit convs: the decoder's
-  // ResidualBlock first convs, ReLU on load + bias + ReLU, no gamma)
-  if (conv) {
-    if (p.gamma) return DP_ERR_ARG;
-    if (p.relu_a) DP_P8(true, true, false);
-    else DP_P8(true, false, false);
-  } else if (p.relu_a) { if (p.gamma) DP_P8(false, true, true); else DP_P8(false, true, false); }
-  else { if (p.gamma) DP_P8(false, false, true); else DP_P8(false, false, false); }
+#define DP_P8(R_, G_) do { \
+    if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_NONE, G_>), grid, dim3(512), 0, s, p); \
+    else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_RELU, G_>), grid, dim3(512), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_GELU, G_>), grid, dim3(512), 0, s, p); } while (0)
+  // (a gamma-free launch -- fc1 -- skips the multiply by 1 per output)
+  if (p.relu_a) { if (p.gamma) DP_P8(true, true); else DP_P8(true, false); }
+  else { if (p.gamma) DP_P8(false, true); else DP_P8(false, false); }
 #undef DP_P8
   DP_CHECK_LAUNCH();
   return 0;
