@@ -33,11 +33,13 @@ PEAK_HBM_GBS = 8000.0
 
 TILE_NAMES = {1: "128x128", 2: "256x64", 3: "256x32", 4: "256x256", 5: "256x128", 8: "8phase-256x256",
               12: "streamK-256x256", 13: "320x256", 14: "512x128", 17: "dual-256x128",
-              18: "persistent-8phase-256x256", 19: "8phase-320x256"}
+              18: "persistent-8phase-256x256", 19: "8phase-320x256",
+              20: "patch-conv3x3-256x256"}
 TILE_KERNEL = {1: "gemm_kernel<{K}, 128, 128", 4: "gemm_big_kernel<{K}, 256, 256", 5: "gemm_big_kernel<{K}, 256, 128",
                8: "gemm_8ph_kernel<{K}", 12: "gemm_sk_kernel<{K}", 13: "gemm_big_kernel<{K}, 320, 256",
                14: "gemm_big_kernel<{K}, 512, 128", 17: "gemm_big_kernel<{K}, 256, 128, 32, 3",
-               18: "gemm_p8ph_kernel<{K}", 19: "gemm_8ph320_kernel<{K}"}
+               18: "gemm_p8ph_kernel<{K}", 19: "gemm_8ph320_kernel<{K}",
+               20: "gemm_cv3_kernel<{K}"}
 
 
 def tile_kernel(tile: int, dtype: torch.dtype) -> str:

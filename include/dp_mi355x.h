@@ -129,13 +129,14 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
        DP_TILE_DEEP5_256x256 = 10, DP_TILE_DEEP_256x128 = 11, DP_TILE_STREAMK_256x256 = 12,
        DP_TILE_BIG_320x256 = 13, DP_TILE_BIG_512x128 = 14, DP_TILE_PBIG_320x256 = 15,
        DP_TILE_PBIG_256x256 = 16, DP_TILE_DUAL_256x128 = 17,
-       DP_TILE_P8PH_256x256 = 18, DP_TILE_8PH_320x256 = 19 };
+       DP_TILE_P8PH_256x256 = 18, DP_TILE_8PH_320x256 = 19, DP_TILE_CV3_256x256 = 20 };
 /* DP_TILE_P8PH_256x256: persistent 8-phase engine (min(tiles, CUs) workgroups, each a stream of
    K steps over its tiles; dense A, N % 256 == 0, K >= 128, 16-bit C without per-row operands);
    the auto choice for the ViT fc1.  DP_TILE_8PH_320x256: 8-phase 320 x 256 engine (dense A, no
    ReLU prologue, N % 256 == 0; 16-bit C without per-row operands, or an fp32 C accumulated into
    without activation); the auto choice for the ViT qkv / proj / fc2.  A hint an engine cannot
-   serve returns DP_ERR_ARG. */
+   serve returns DP_ERR_ARG.  DP_TILE_CV3_256x256: stride-1 pad-1 3x3 implicit conv on 16 x 16 pixel
+   tiles with the input patch in LDS (square maps, side % 16 == 0, in_c % 64 == 0, N % 256 == 0). */
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 

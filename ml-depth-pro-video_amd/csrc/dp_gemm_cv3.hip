@@ -1,0 +1,225 @@
+// dp_gemm_cv3.hip: the 3x3 patch-conv engine -- a stride-1, pad-1 3x3 implicit-GEMM conv on
+// output tiles of 16 x 16 pixels x 256 channels whose input patch (18 x 18 pixels, one 64-channel
+// block) sits in LDS, so the 9 taps of a channel block read their A fragments from the patch
+// instead of streaming 9 shifted 256-pixel slices from L2.
+//
+// Why: the row-raster implicit conv (the big / persistent engines) moves 64 KiB per K step
+// (256 shifted pixel rows + 256 weight rows); on the decoder's 768^2 convs that load stream
+// alone takes as long as the MFMAs (tools/gemm_bench.py --ablate: 364 vs 393 us) and the two
+// overlap poorly.  Here a K step moves the 32 KiB weight tile plus 1/9 of a 48 KiB patch.
+//
+// Layout: 8 waves as 2 (M) x 4 (N), wave tile 128 x 64 = 8 output pixel rows of the tile x 16
+// pixels; K order (channel block, tap, 64 channels) = the packed conv weights
+// ([Cout][Cin/64][ky][kx][64], ops.conv_weight).  LDS: 2 patch buffers (48 LDS-DMA pieces of
+// 1 KiB each: 324 pixels x 128 B, the 16-B chunk XOR-swizzled by pixel index, 7 dummy pieces
+// so every wave issues 6) + a 2-stage ring of weight K steps = 160 KiB.  One barrier per K step:
+// the weight tile of step t+1 and (at a channel block's first tap) the next block's patch are
+// issued right after it, the counted wait at the top of the next step retires them.  The
+// epilogue (bias, ReLU, residuals R1 / R2, 16-bit C) works in the MFMA register layout, one
+// 16-pixel output row segment per fragment row.
+#include "dp_gemm_impl.h"
+
+namespace {
+
+constexpr int CV_T = 16;                      // output tile side (pixels)
+constexpr int CV_P = CV_T + 2;                // patch side
+constexpr int CV_PIX = CV_P * CV_P;           // 324 patch pixels
+constexpr int CV_PIECES = 48;                 // 6 per wave; pieces 41-47 only hold zero-page reads
+constexpr int CV_PATCH_B = CV_PIECES * 1024;  // bytes per patch buffer
+constexpr int CV_B_B = 256 * 128;             // bytes per weight K step (256 rows x 64 x 16-bit)
+
+template <typename K_, bool RELU>
+__global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
+  constexpr int FM = 8, FN = 4, TN = 64;   // wave tile 128 x 64
+  __shared__ __attribute__((aligned(1024))) char smem[2 * CV_PATCH_B + 2 * CV_B_B];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  // XCD-contiguous: an XCD's workgroups are consecutive tiles of a tile row (shared halos)
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int S = p.out_w, tpr = S / CV_T, tpi = tpr * tpr;
+  const int tn = wgid % p.tiles_n, sp = wgid / p.tiles_n;
+  const int img = sp / tpi, r_ = sp - img * tpi;
+  const int y0 = (r_ / tpr) * CV_T, x0 = (r_ % tpr) * CV_T, n0 = tn * 256;
+  const int cin = p.in_c, CB = cin / 64;
+  const int KT = CB * 9;
+
+  // patch pieces of this lane: element offset of its 16-B chunk (channel block 0), or -1 when
+  // the pixel is in the zero padding or past the patch
+  int poff[6];
+  #pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int c = (wave * 6 + i) * 64 + lane;   // chunk index in the patch image
+    const int P = c >> 3, slot = c & 7;
+    int off = -1;
+    if (P < CV_PIX) {
+      const int pr = P / CV_P, pc = P - pr * CV_P;
+      const int iy = y0 - 1 + pr, ix = x0 - 1 + pc;
+      if ((unsigned)iy < (unsigned)S && (unsigned)ix < (unsigned)S)
+        off = ((img * S + iy) * S + ix) * cin + ((slot ^ (P & 7)) << 3);
+    }
+    poff[i] = off;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  auto issue_patch = [&](int cb, int buf) {
+    const uint32_t dst = lds0 + buf * CV_PATCH_B + wave_u * 6 * 1024;
+    #pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const void* src = poff[i] >= 0 ? (const void*)(p.A + (poff[i] + cb * 64)) : (const void*)g_zero_page;
+      glds16(src, dst + i * 1024);
+    }
+  };
+  // weight K step t: rows n0 + i*64 + wave*8 + lane/8, chunk swizzled on the source (as gemm_big_kernel)
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  int boff[4];
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) boff[i] = (n0 + i * 64 + prow) * (int)p.ldb + pchunk * 8;
+  auto issue_b = [&](int t, int st) {
+    const uint32_t dst = lds0 + 2 * CV_PATCH_B + st * CV_B_B + wave_u * 1024;
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(p.B + (boff[i] + t * 64), dst + i * 8192);
+  };
+
+  f32x4_t acc[FM][FN];
+  #pragma unroll
+  for (int i = 0; i < FM; ++i)
+    #pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int frow = lane & 15, fchunk = lane >> 4;
+  auto compute = [&](int t) {
+    const int cb = t / 9, tap = t - cb * 9, ky = tap / 3, kx = tap - ky * 3;
+    const char* pa = smem + (cb & 1) * CV_PATCH_B;
+    const u16* sb = (const u16*)(smem + 2 * CV_PATCH_B + (t & 1) * CV_B_B);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 bf[FN];
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = *(const uint4*)(sb + lds_off(wn * TN + j * 16 + frow, ks * 4 + fchunk));
+      uint4 afs[FM];
+      #pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        // output pixel (wm * 8 + i, frow) of the tile -> patch pixel (+ky, +kx)
+        const int P = (wm * 8 + i + ky) * CV_P + frow + kx;
+        afs[i] = *(const uint4*)(pa + P * 128 + (((ks * 4 + fchunk) ^ (P & 7)) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+      #pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        uint4 af = afs[i];
+        if constexpr (RELU) af = relu_pk16(af);
+        #pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  // prologue: channel block 0's patch and weight step 0
+  issue_patch(0, 0);
+  issue_b(0, 0);
+  wait_vmcnt<0>();
+  lds_barrier();
+  for (int t = 0; t < KT; ++t) {
+    if (t > 0) {
+      // weight step t landed (and, at a block's first tap, its patch: issued 9 steps earlier);
+      // younger: the next block's patch when step t-1 issued one
+      const int pt = t - 1;
+      if (pt % 9 == 0 && pt / 9 + 1 < CB) wait_vmcnt<6>(); else wait_vmcnt<0>();
+      lds_barrier();
+    }
+    if (t + 1 < KT) issue_b(t + 1, (t + 1) & 1);
+    if (t % 9 == 0 && t / 9 + 1 < CB) issue_patch(t / 9 + 1, (t / 9 + 1) & 1);
+    compute(t);
+  }
+
+  // epilogue in the MFMA register layout: fragment row fm of the wave is output pixel row
+  // wm * 8 + fm of the tile (16 consecutive pixels), each lane 4 consecutive channels.  bias,
+  // activation, residuals R1 / R2 (loaded one fragment row ahead) in epilogue_rows' order (bit-
+  // identical), packed to 16 bits, staged through the wave's 2 KiB LDS slab and stored as whole
+  // 128-B row segments (2 stores per lane per fragment row).  16-bit C, no gamma / pos /
+  // accumulate (host checks).
+  lds_barrier();   // the ring is free once every wave has left the K loop
+  char* slab = smem + wave * 2048;
+  const int t = lane & 15, g = lane >> 4;
+  const int nw = n0 + wn * TN;
+  f32x4_t bias[FN];
+  #pragma unroll
+  for (int fn = 0; fn < FN; ++fn)
+    bias[fn] = p.bias ? *(const f32x4_t*)(p.bias + nw + fn * 16 + 4 * g) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto mrow = [&](int fm) { return (long long)((img * S + y0 + wm * 8 + fm) * S + x0); };
+  uint2 r1c[FN], r2c[FN], r1n[FN], r2n[FN];
+  auto loadr = [&](int fm, uint2 (&r1)[FN], uint2 (&r2)[FN]) __attribute__((always_inline)) {
+    const long long m = mrow(fm) + t;
+    #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int col = nw + fn * 16 + 4 * g;
+      if (p.R1) r1[fn] = *(const uint2*)(p.R1 + m * p.ldr1 + col);
+      if (p.R2) r2[fn] = *(const uint2*)(p.R2 + m * p.ldr2 + col);
+    }
+  };
+  auto addr = [&](f32x4_t& x, uint2 r) __attribute__((always_inline)) {
+    x[0] += K_::to_f(r.x & 0xffff); x[1] += K_::to_f(r.x >> 16);
+    x[2] += K_::to_f(r.y & 0xffff); x[3] += K_::to_f(r.y >> 16);
+  };
+  loadr(0, r1c, r2c);
+  #pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    if (fm + 1 < FM) loadr(fm + 1, r1n, r2n);
+    #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      f32x4_t x = acc[fm][fn] + bias[fn];
+      if (p.act == DP_ACT_RELU) {
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = fmaxf(x[r], 0.f);
+      }
+      if (p.R1) addr(x, r1c[fn]);
+      if (p.R2) addr(x, r2c[fn]);
+      const int chunk = fn * 2 + (g >> 1);
+      uint2 w;
+      w.x = K_::pack2(x[0], x[1]);
+      w.y = K_::pack2(x[2], x[3]);
+      *(uint2*)(slab + t * 128 + ((chunk ^ (t & 7)) << 4) + (g & 1) * 8) = w;
+    }
+    #pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int row = k * 8 + (lane >> 3), chunk = lane & 7;
+      const uint4 d = *(const uint4*)(slab + row * 128 + ((chunk ^ (row & 7)) << 4));
+      *(uint4*)((u16*)p.C + (mrow(fm) + row) * p.ldc + nw + chunk * 8) = d;
+    }
+    #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) { r1c[fn] = r1n[fn]; r2c[fn] = r2n[fn]; }
+  }
+}
+
+template <typename K_>
+int launch_cv3(const GemmP& p0, hipStream_t s) {
+  GemmP p = p0;
+  const int S = p.out_w;
+  if (p.k_h != 3 || p.k_w != 3 || p.stride != 1 || p.pad != 1 || p.in_h != S || p.in_w != S || p.out_h != S ||
+      S % CV_T || p.in_c % 64 || p.N % 256 || p.M % (S * S) || p.store_mode != DP_STORE_ROWS || p.row_group ||
+      p.head_w || p.head_corr || p.c_dtype == DP_F32 || p.gamma || p.pos || p.accumulate ||
+      (p.act != DP_ACT_NONE && p.act != DP_ACT_RELU))
+    return DP_ERR_ARG;
+  if ((long long)p.M * p.in_c >= (1LL << 31) || (long long)p.N * p.ldb >= (1LL << 31)) return DP_ERR_ARG;
+  p.tiles_n = p.N / 256;
+  p.tiles_m = (p.M / (S * S)) * (S / CV_T) * (S / CV_T);
+  dim3 grid(p.tiles_m * p.tiles_n);
+  if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true>), grid, dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false>), grid, dim3(512), 0, s, p);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+namespace dpg {
+int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s) {
+  if (!conv) return DP_ERR_ARG;
+  return bf16 ? launch_cv3<KBF16>(p, s) : launch_cv3<KF16>(p, s);
+}
+}  // namespace dpg

@@ -97,6 +97,7 @@ int launch_part_big(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t 
 int launch_part_big320(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);   // dp_gemm_big320.hip
 int launch_part_8ph(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);      // dp_gemm_8ph.hip
 int launch_part_8ph320(const GemmP& p, bool conv, bool bf16, hipStream_t s);             // dp_gemm_8ph320.hip
+int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s);                // dp_gemm_cv3.hip
 int launch_part_pbig(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);     // dp_gemm_pbig.hip
 int launch_part_small(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);    // dp_gemm_small.hip
 int launch_part_sk(const GemmP& p, bool conv, void* ws, bool bf16, hipStream_t s);       // dp_gemm_sk.hip

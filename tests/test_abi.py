@@ -102,3 +102,6 @@ def test_gemm_plan_tile_choice():
     assert conv(192, 512, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 256)       # 144 tiles over 256 CUs
     assert conv(48, 1024)[1] != _lib.DP_TILE_STREAMK_256x256                        # no workspace
     assert conv(48, 256, **wsk)[1] == _lib.DP_TILE_BIG_256x128                     # K = 2304
+    # the 768^2 ResidualBlock convs (2304 tiles of 256 pixels): the 3x3 patch-conv engine; 384^2 not
+    assert conv(768, 256, **wsk)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
+    assert conv(384, 256, **wsk)[1] != _lib.DP_TILE_CV3_256x256

@@ -703,3 +703,39 @@ def test_8phase_320_bit_identical_to_320(cuda, dt, case):
     torch.cuda.synchronize()
     assert torch.equal(C1, C2), (C1.float() - C2.float()).abs().max().item()
     close(C1, ref, cdt, f"8ph320 {case}")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("case", ["relu_bias_relu", "residual2", "cin128_n512"])
+def test_patch_conv3x3_bit_identical(cuda, dt, case):
+    """The 3x3 patch-conv engine (DP_TILE_CV3_256x256: 16 x 16 pixel tiles, the input patch of a
+    channel block in LDS, the 9 taps read from it) gives exactly the 256 x 256 big engine's result
+    -- same K order, same zero padding, same epilogue -- for the decoder ResidualBlock convs (ReLU
+    on load + bias + ReLU; bias + two residuals), 2 images, a wider N; and matches F.conv2d."""
+    from depth_pro._lib import DP_TILE_CV3_256x256
+
+    g = torch.Generator().manual_seed(sum(map(ord, case)))
+    S, Ci, Co, nb = {"relu_bias_relu": (96, 256, 256, 1), "residual2": (64, 256, 256, 2),
+                     "cin128_n512": (48, 128, 512, 1)}[case]
+    x = rnd(nb, Ci, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(Co, Ci, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * Ci) ** -0.5)
+    b = torch.randn(Co, generator=g).to(cuda)
+    xh = x.permute(0, 2, 3, 1).reshape(nb * S * S, Ci).contiguous()
+    kw = dict(M=nb * S * S, N=Co, K=9 * Ci, conv=dict(in_h=S, in_w=S, in_c=Ci, k=3, stride=1, pad=1, out_h=S, out_w=S),
+              bias=b)
+    ref = F.conv2d(x.float(), w.float(), b, padding=1)
+    if case == "relu_bias_relu":
+        kw.update(relu_a=True, act=DP_ACT_RELU)
+        ref = F.relu(F.conv2d(F.relu(x.float()), w.float(), b, padding=1))
+    elif case == "residual2":
+        r1 = rnd(nb * S * S, Co, dt=dt, dev=cuda, gen=g)
+        r2 = rnd(nb * S * S, Co, dt=dt, dev=cuda, gen=g)
+        kw.update(R1=r1, ldr1=Co, R2=r2, ldr2=Co)
+        ref = ref + (r1.float() + r2.float()).reshape(nb, S, S, Co).permute(0, 3, 1, 2)
+    out1 = torch.full((nb * S * S, Co), 7.0, dtype=dt, device=cuda)
+    out2 = out1.clone()
+    ops.gemm(xh, ops.conv_weight(w), out1, tile=DP_TILE_CV3_256x256, **kw)
+    ops.gemm(xh, ops.conv_weight(w), out2, tile=DP_TILE_BIG_256x256, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max().item()
+    close(out1.reshape(nb, S, S, Co).permute(0, 3, 1, 2), ref, dt, f"cv3 {case}")
