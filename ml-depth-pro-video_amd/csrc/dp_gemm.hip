@@ -219,14 +219,14 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     if (plain && epi_ok) tile = DP_TILE_8PH_320x256;
   }
   // the 3x3 patch-conv engine for the many-round stride-1 3x3 convs (the decoder's 768^2
-  // ResidualBlock convs: 722 -> 649 us in-frame, 45.14 / 45.08 -> 45.68 / 45.80 fps,
-  // profiles/r03s_cv3/; debug 1 << 16: off)
+  // ResidualBlock convs: 722 -> 641 - 652 us in-frame, 45.30 / 45.41 -> 46.17 / 46.04 fps,
+  // profiles/r03s_cv3/, r03u_cv3_8ph/; debug 1 << 16: off)
   if (a->tile == DP_TILE_AUTO && !(dbg & (1 << 16)) && a->a_mode == DP_A_CONV && a->k_h == 3 && a->k_w == 3 &&
       a->stride == 1 && a->pad == 1 && a->in_h == a->in_w && a->out_h == a->in_h && a->out_w == a->in_w &&
       a->in_w % 16 == 0 && a->in_c % 64 == 0 && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
       !a->row_group && !a->head_w && !a->head_corr && (long long)a->M * a->in_c < (1LL << 31) &&
       a->c_dtype != DP_F32 && !a->gamma && !a->pos && !a->accumulate && a->act != DP_ACT_GELU &&
-      (long long)(a->M / 256) * (a->N / 256) >= 4LL * num_cus())   // many rounds (the 768^2 maps)
+      (long long)(a->M / 256) * (a->N / 256) >= 4LL * num_cus())   // many rounds (the 768^2 maps; 384^2: 201 vs 185 us)
     tile = DP_TILE_CV3_256x256;
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
   // the border-corrected composed conv exists in the 512 x 128 conv engine only

@@ -12,9 +12,9 @@
 // pixels; K order (channel block, tap, 64 channels) = the packed conv weights
 // ([Cout][Cin/64][ky][kx][64], ops.conv_weight).  LDS: 2 patch buffers (48 LDS-DMA pieces of
 // 1 KiB each: 324 pixels x 128 B, the 16-B chunk XOR-swizzled by pixel index, 7 dummy pieces
-// so every wave issues 6) + a 2-stage ring of weight K steps = 160 KiB.  One barrier per K step:
-// the weight tile of step t+1 and (at a channel block's first tap) the next block's patch are
-// issued right after it, the counted wait at the top of the next step retires them.  The
+// so every wave issues 6) + a 2-stage ring of weight K steps = 160 KiB.  The K loop is the
+// 8-phase schedule of gemm_8ph_kernel (two wave groups staggered by one barrier, one LDS-DMA
+// group per phase, one counted wait per step) with the A fragments read from the patch.  The
 // epilogue (bias, ReLU, residuals R1 / R2, 16-bit C) works in the MFMA register layout, one
 // 16-pixel output row segment per fragment row.
 #include "dp_gemm_impl.h"
@@ -65,24 +65,29 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     poff[i] = off;
   }
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
-  auto issue_patch = [&](int cb, int buf) {
+
+  // weight K step t in the 8-phase layout (gemm_8ph_kernel): two halves of 128 rows (output
+  // channels), 16 KiB each; half h rows h*128 + i*64 + wave*8 + lane/8, chunk swizzled on the source
+  constexpr int HALF = 128 * 128;
+  const int prow = wave * 8 + (lane >> 3);
+  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
+  int boff[2][2];
+  #pragma unroll
+  for (int h = 0; h < 2; ++h)
+    #pragma unroll
+    for (int i = 0; i < 2; ++i) boff[h][i] = (n0 + h * 128 + i * 64 + prow) * (int)p.ldb + pchunk * 8;
+  auto issue_b = [&](int h, int t) {   // half h of weight step t -> stage t & 1
+    const uint32_t dst = lds0 + 2 * CV_PATCH_B + (t & 1) * CV_B_B + h * HALF + wave_u * 1024;
+    #pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(p.B + (boff[h][i] + t * 64), dst + i * 8192);
+  };
+  auto issue_patch3 = [&](int cb, int buf, int i0) {   // 3 of the wave's 6 patch pieces
     const uint32_t dst = lds0 + buf * CV_PATCH_B + wave_u * 6 * 1024;
     #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int i = i0; i < i0 + 3; ++i) {
       const void* src = poff[i] >= 0 ? (const void*)(p.A + (poff[i] + cb * 64)) : (const void*)g_zero_page;
       glds16(src, dst + i * 1024);
     }
-  };
-  // weight K step t: rows n0 + i*64 + wave*8 + lane/8, chunk swizzled on the source (as gemm_big_kernel)
-  const int prow = wave * 8 + (lane >> 3);
-  const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
-  int boff[4];
-  #pragma unroll
-  for (int i = 0; i < 4; ++i) boff[i] = (n0 + i * 64 + prow) * (int)p.ldb + pchunk * 8;
-  auto issue_b = [&](int t, int st) {
-    const uint32_t dst = lds0 + 2 * CV_PATCH_B + st * CV_B_B + wave_u * 1024;
-    #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(p.B + (boff[i] + t * 64), dst + i * 8192);
   };
 
   f32x4_t acc[FM][FN];
@@ -91,51 +96,82 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int frow = lane & 15, fchunk = lane >> 4;
-  auto compute = [&](int t) {
-    const int cb = t / 9, tap = t - cb * 9, ky = tap / 3, kx = tap - ky * 3;
-    const char* pa = smem + (cb & 1) * CV_PATCH_B;
-    const u16* sb = (const u16*)(smem + 2 * CV_PATCH_B + (t & 1) * CV_B_B);
+  uint4 af[2][4], bf[2][2][2];
+  // quadrant qm of the wave tile = output pixel rows wm*8 + qm*4 .. +3; tap (ky, kx) of patch buffer pb
+  auto readA = [&](int qm, int pb, int ky, int kx) {
+    const char* pa = smem + pb * CV_PATCH_B;
     #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      uint4 bf[FN];
+    for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = *(const uint4*)(sb + lds_off(wn * TN + j * 16 + frow, ks * 4 + fchunk));
-      uint4 afs[FM];
-      #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        // output pixel (wm * 8 + i, frow) of the tile -> patch pixel (+ky, +kx)
-        const int P = (wm * 8 + i + ky) * CV_P + frow + kx;
-        afs[i] = *(const uint4*)(pa + P * 128 + (((ks * 4 + fchunk) ^ (P & 7)) << 4));
+      for (int fm = 0; fm < 4; ++fm) {
+        const int P = (wm * 8 + qm * 4 + fm + ky) * CV_P + frow + kx;
+        af[ks][fm] = *(const uint4*)(pa + P * 128 + (((ks * 4 + fchunk) ^ (P & 7)) << 4));
       }
-      __builtin_amdgcn_s_setprio(1);
-      #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        uint4 af = afs[i];
-        if constexpr (RELU) af = relu_pk16(af);
-        #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
-      }
-      __builtin_amdgcn_s_setprio(0);
-    }
   };
+  auto readB = [&](int qn, int st) {
+    const u16* sb = (const u16*)(smem + 2 * CV_PATCH_B + st * CV_B_B + (wn >> 1) * HALF);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fn = 0; fn < 2; ++fn)
+        bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((wn & 1) * 64 + qn * 32 + fn * 16 + frow, ks * 4 + fchunk));
+  };
+  auto mma = [&](int qm, int qn) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      #pragma unroll
+      for (int fm = 0; fm < 4; ++fm) {
+        uint4 a = af[ks][fm];
+        if constexpr (RELU) a = relu_pk16(a);
+        #pragma unroll
+        for (int fn = 0; fn < 2; ++fn)
+          acc[qm * 4 + fm][qn * 2 + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * 2 + fn]);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
 
-  // prologue: channel block 0's patch and weight step 0
-  issue_patch(0, 0);
-  issue_b(0, 0);
-  wait_vmcnt<0>();
+  // The 8-phase schedule of gemm_8ph_kernel, A from the patch: per K step (channel block cb,
+  // tap) four quadrant phases {fragment reads, LDS-DMA, s_barrier, 16 MFMAs, s_barrier}; reads
+  // p0 A(qm0) + B(qn0), p1 B(qn1), p2 A(qm1); weight halves of step t+2 in phases 2 / 3 (their
+  // stage's weight reads ended in phase 1), the next block's patch in phases 0 / 1 of a block's
+  // first step (its buffer was last read two phases earlier); wave rows staggered by a barrier;
+  // one counted wait per step (phase 3) for step t+1.
+  // prologue: patch of block 0 and weight steps 0 and 1
+  issue_patch3(0, 0, 0); issue_patch3(0, 0, 3);
+  issue_b(0, 0); issue_b(1, 0);
+  if (KT > 1) { issue_b(0, 1); issue_b(1, 1); wait_vmcnt<4>(); } else { wait_vmcnt<0>(); }
   lds_barrier();
+  if (wm == 1) bar();
   for (int t = 0; t < KT; ++t) {
-    if (t > 0) {
-      // weight step t landed (and, at a block's first tap, its patch: issued 9 steps earlier);
-      // younger: the next block's patch when step t-1 issued one
-      const int pt = t - 1;
-      if (pt % 9 == 0 && pt / 9 + 1 < CB) wait_vmcnt<6>(); else wait_vmcnt<0>();
-      lds_barrier();
-    }
-    if (t + 1 < KT) issue_b(t + 1, (t + 1) & 1);
-    if (t % 9 == 0 && t / 9 + 1 < CB) issue_patch(t / 9 + 1, (t / 9 + 1) & 1);
-    compute(t);
+    const int cb = t / 9, tap = t - cb * 9, ky = tap / 3, kx = tap - ky * 3;
+    const int pb = cb & 1, st = t & 1;
+    const bool np = tap == 0 && cb + 1 < CB;    // this step streams the next block's patch
+    const bool n2 = t + 2 < KT;
+    // phase 0: quadrant (0,0)
+    readA(0, pb, ky, kx); readB(0, st);
+    if (np) issue_patch3(cb + 1, pb ^ 1, 0);
+    bar(); mma(0, 0); bar();
+    // phase 1: quadrant (0,1)
+    readB(1, st);
+    if (np) issue_patch3(cb + 1, pb ^ 1, 3);
+    bar(); mma(0, 1); bar();
+    // phase 2: quadrant (1,0)
+    readA(1, pb, ky, kx);
+    if (n2) issue_b(0, t + 2);
+    bar(); mma(1, 0); bar();
+    // phase 3: quadrant (1,1); weight step t+1 (and a next block's patch) landed before this
+    // phase's first barrier -- younger: this step's patch pieces and the first half of step t+2
+    if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
+    else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
+    if (n2) issue_b(1, t + 2);
+    bar(); mma(1, 1);
+    bar();
   }
+  if (wm == 0) bar();
 
   // epilogue in the MFMA register layout: fragment row fm of the wave is output pixel row
   // wm * 8 + fm of the tile (16 consecutive pixels), each lane 4 consecutive channels.  bias,
