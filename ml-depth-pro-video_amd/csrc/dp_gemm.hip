@@ -110,8 +110,12 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   const int dbg = g_dbg_flags.load(std::memory_order_relaxed);
   tile = a->tile;
   if (a->store_mode == DP_STORE_HEAD_PS) {
-    // 32-column parity groups must not straddle a wave's columns (TN = 32 or 64)
-    tile = a->M >= 512 * 256 ? DP_TILE_BIG_512x128 : DP_TILE_BIG_256x128;
+    // 32-column parity groups must not straddle a wave's columns (TN = 32 or 64); the patch-conv
+    // engine (one parity per wave) when asked for, or for maps it tiles (A/B: debug 4096 = off)
+    const bool cv3 = a->in_w % 16 == 0 && a->in_h == a->in_w && a->M >= 512 * 256 && a->in_c % 64 == 0 &&
+                     a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 && !(dbg & 4096);
+    if (tile == DP_TILE_AUTO && cv3) tile = DP_TILE_CV3_256x256;
+    else if (tile != DP_TILE_CV3_256x256) tile = a->M >= 512 * 256 ? DP_TILE_BIG_512x128 : DP_TILE_BIG_256x128;
   } else if (a->head_w) {
     if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;
     tile = DP_TILE_256x32;
@@ -122,7 +126,15 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     if (a->N <= 32) tile = DP_TILE_256x32;
     else if (a->N <= 64) tile = DP_TILE_256x64;
     else if (a->N % 8 != 0) tile = DP_TILE_128x128;
-    else if (a->N == 128 && a->M >= 512 * 256) tile = DP_TILE_BIG_512x128;   // N = 128 convs at 768^2
+    else if (a->N == 128 && a->M >= 512 * 256) {   // N = 128 convs at 768^2: the head.0 conv
+      // the patch-conv engine for the stride-1 square ones (the composed out_conv∘head.0); A/B:
+      // debug 4096 = the 512 x 128 engine
+      const bool cv3 = a->a_mode == DP_A_CONV && a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 &&
+                       a->in_h == a->in_w && a->out_h == a->in_h && a->out_w == a->in_w && a->in_w % 16 == 0 &&
+                       a->in_c % 64 == 0 && a->head_corr && a->store_mode == DP_STORE_ROWS && a->c_dtype != DP_F32 &&
+                       !a->R1 && !a->R2 && !a->gamma && !a->pos && !a->accumulate && !a->row_group && !(dbg & 4096);
+      tile = cv3 ? DP_TILE_CV3_256x256 : DP_TILE_BIG_512x128;
+    }
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
     else if (ws_ok && a->a_mode == DP_A_CONV && !(dbg & 32) && tiles256 < num_cus() &&
              a->K >= 4608) {
@@ -230,7 +242,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     tile = DP_TILE_CV3_256x256;
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
   // the border-corrected composed conv exists in the 512 x 128 conv engine only
-  if (a->store_mode == DP_STORE_ROWS && a->head_corr && tile != DP_TILE_BIG_512x128) return DP_ERR_ARG;
+  if (a->store_mode == DP_STORE_ROWS && a->head_corr && tile != DP_TILE_BIG_512x128 && tile != DP_TILE_CV3_256x256)
+    return DP_ERR_ARG;
 
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;

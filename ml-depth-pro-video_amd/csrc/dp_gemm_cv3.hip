@@ -26,12 +26,20 @@ constexpr int CV_P = CV_T + 2;                // patch side
 constexpr int CV_PIX = CV_P * CV_P;           // 324 patch pixels
 constexpr int CV_PIECES = 48;                 // 6 per wave; pieces 41-47 only hold zero-page reads
 constexpr int CV_PATCH_B = CV_PIECES * 1024;  // bytes per patch buffer
-constexpr int CV_B_B = 256 * 128;             // bytes per weight K step (256 rows x 64 x 16-bit)
 
-template <typename K_, bool RELU>
+// BN: output channels per tile (256: the ResidualBlock convs; 128: the head convs).  EPI:
+// CV_EPI_RES (bias, ReLU, residuals; BN 256), CV_EPI_BC (bias + the composed conv's border-tap
+// correction, DP_STORE_ROWS with head_corr), CV_EPI_HPS (the composed depth head's pixel-shuffle
+// + 1x1 epilogue, DP_STORE_HEAD_PS; BN 128: one output parity per wave).
+constexpr int CV_EPI_RES = 0, CV_EPI_BC = 1, CV_EPI_HPS = 2;
+template <typename K_, bool RELU, int BN, int EPI>
 __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
-  constexpr int FM = 8, FN = 4, TN = 64;   // wave tile 128 x 64
-  __shared__ __attribute__((aligned(1024))) char smem[2 * CV_PATCH_B + 2 * CV_B_B];
+  constexpr int FM = 8, TN = BN / 4, FN = TN / 16, QF = FN / 2;   // wave tile 128 x TN
+  constexpr int NBH = BN / 128;                                  // weight halves per K step
+  constexpr int B_B = BN * 128;                                  // bytes per weight K step
+  static_assert(EPI != CV_EPI_RES || BN == 256, "residual epilogue: BN 256");
+  static_assert(EPI != CV_EPI_HPS || BN == 128, "head epilogue: one parity (32 columns) per wave");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * CV_PATCH_B + 2 * B_B];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6;
@@ -44,7 +52,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   const int S = p.out_w, tpr = S / CV_T, tpi = tpr * tpr;
   const int tn = wgid % p.tiles_n, sp = wgid / p.tiles_n;
   const int img = sp / tpi, r_ = sp - img * tpi;
-  const int y0 = (r_ / tpr) * CV_T, x0 = (r_ % tpr) * CV_T, n0 = tn * 256;
+  const int y0 = (r_ / tpr) * CV_T, x0 = (r_ % tpr) * CV_T, n0 = tn * BN;
   const int cin = p.in_c, CB = cin / 64;
   const int KT = CB * 9;
 
@@ -66,18 +74,18 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   }
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
 
-  // weight K step t in the 8-phase layout (gemm_8ph_kernel): two halves of 128 rows (output
+  // weight K step t in the 8-phase layout (gemm_8ph_kernel): NBH halves of 128 rows (output
   // channels), 16 KiB each; half h rows h*128 + i*64 + wave*8 + lane/8, chunk swizzled on the source
   constexpr int HALF = 128 * 128;
   const int prow = wave * 8 + (lane >> 3);
   const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
-  int boff[2][2];
+  int boff[NBH][2];
   #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < NBH; ++h)
     #pragma unroll
     for (int i = 0; i < 2; ++i) boff[h][i] = (n0 + h * 128 + i * 64 + prow) * (int)p.ldb + pchunk * 8;
   auto issue_b = [&](int h, int t) {   // half h of weight step t -> stage t & 1
-    const uint32_t dst = lds0 + 2 * CV_PATCH_B + (t & 1) * CV_B_B + h * HALF + wave_u * 1024;
+    const uint32_t dst = lds0 + 2 * CV_PATCH_B + (t & 1) * B_B + h * HALF + wave_u * 1024;
     #pragma unroll
     for (int i = 0; i < 2; ++i) glds16(p.B + (boff[h][i] + t * 64), dst + i * 8192);
   };
@@ -96,7 +104,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int frow = lane & 15, fchunk = lane >> 4;
-  uint4 af[2][4], bf[2][2][2];
+  uint4 af[2][4], bf[2][2][QF];
   // quadrant qm of the wave tile = output pixel rows wm*8 + qm*4 .. +3; tap (ky, kx) of patch buffer pb
   auto readA = [&](int qm, int pb, int ky, int kx) {
     const char* pa = smem + pb * CV_PATCH_B;
@@ -108,13 +116,14 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
         af[ks][fm] = *(const uint4*)(pa + P * 128 + (((ks * 4 + fchunk) ^ (P & 7)) << 4));
       }
   };
-  auto readB = [&](int qn, int st) {
-    const u16* sb = (const u16*)(smem + 2 * CV_PATCH_B + st * CV_B_B + (wn >> 1) * HALF);
+  auto readB = [&](int qn, int st) {   // columns wn*TN + qn*TN/2 .. of the tile
+    const int c0 = wn * TN + qn * (TN / 2);
+    const u16* sb = (const u16*)(smem + 2 * CV_PATCH_B + st * B_B + (c0 >> 7) * HALF);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
-      for (int fn = 0; fn < 2; ++fn)
-        bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((wn & 1) * 64 + qn * 32 + fn * 16 + frow, ks * 4 + fchunk));
+      for (int fn = 0; fn < QF; ++fn)
+        bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((c0 & 127) + fn * 16 + frow, ks * 4 + fchunk));
   };
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -127,8 +136,8 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
         uint4 a = af[ks][fm];
         if constexpr (RELU) a = relu_pk16(a);
         #pragma unroll
-        for (int fn = 0; fn < 2; ++fn)
-          acc[qm * 4 + fm][qn * 2 + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * 2 + fn]);
+        for (int fn = 0; fn < QF; ++fn)
+          acc[qm * 4 + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * QF + fn]);
       }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -142,8 +151,15 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   // one counted wait per step (phase 3) for step t+1.
   // prologue: patch of block 0 and weight steps 0 and 1
   issue_patch3(0, 0, 0); issue_patch3(0, 0, 3);
-  issue_b(0, 0); issue_b(1, 0);
-  if (KT > 1) { issue_b(0, 1); issue_b(1, 1); wait_vmcnt<4>(); } else { wait_vmcnt<0>(); }
+  #pragma unroll
+  for (int h = 0; h < NBH; ++h) issue_b(h, 0);
+  if (KT > 1) {
+    #pragma unroll
+    for (int h = 0; h < NBH; ++h) issue_b(h, 1);
+    wait_vmcnt<2 * NBH>();
+  } else {
+    wait_vmcnt<0>();
+  }
   lds_barrier();
   if (wm == 1) bar();
   for (int t = 0; t < KT; ++t) {
@@ -165,22 +181,20 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     bar(); mma(1, 0); bar();
     // phase 3: quadrant (1,1); weight step t+1 (and a next block's patch) landed before this
     // phase's first barrier -- younger: this step's patch pieces and the first half of step t+2
+    // (BN 128: its only half)
     if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
     else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
-    if (n2) issue_b(1, t + 2);
+    if (NBH == 2 && n2) issue_b(NBH - 1, t + 2);
     bar(); mma(1, 1);
     bar();
   }
   if (wm == 0) bar();
 
-  // epilogue in the MFMA register layout: fragment row fm of the wave is output pixel row
-  // wm * 8 + fm of the tile (16 consecutive pixels), each lane 4 consecutive channels.  bias,
-  // activation, residuals R1 / R2 (loaded one fragment row ahead) in epilogue_rows' order (bit-
-  // identical), packed to 16 bits, staged through the wave's 2 KiB LDS slab and stored as whole
-  // 128-B row segments (2 stores per lane per fragment row).  16-bit C, no gamma / pos /
-  // accumulate (host checks).
+  // epilogues in the MFMA register layout: fragment row fm of the wave is output pixel row
+  // wm * 8 + fm of the tile (16 consecutive pixels, lane & 15), each lane 4 consecutive
+  // channels per fragment column (fn * 16 + 4 (lane >> 4)).  Same operations in the same order as
+  // epilogue_rows / head_ps_rows: bit-identical to the row-raster engines.
   lds_barrier();   // the ring is free once every wave has left the K loop
-  char* slab = smem + wave * 2048;
   const int t = lane & 15, g = lane >> 4;
   const int nw = n0 + wn * TN;
   f32x4_t bias[FN];
@@ -188,47 +202,115 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   for (int fn = 0; fn < FN; ++fn)
     bias[fn] = p.bias ? *(const f32x4_t*)(p.bias + nw + fn * 16 + 4 * g) : f32x4_t{0.f, 0.f, 0.f, 0.f};
   auto mrow = [&](int fm) { return (long long)((img * S + y0 + wm * 8 + fm) * S + x0); };
-  uint2 r1c[FN], r2c[FN], r1n[FN], r2n[FN];
-  auto loadr = [&](int fm, uint2 (&r1)[FN], uint2 (&r2)[FN]) __attribute__((always_inline)) {
-    const long long m = mrow(fm) + t;
+  if constexpr (EPI == CV_EPI_HPS) {
+    // composed depth head (head_ps_rows): this wave's 32 columns are parity q = wn of output
+    // channels o = fn * 16 + 4 g + r; z = acc + bias - border taps of head.2's zero padding,
+    // ReLU, dot with head.4 (32), + b, ReLU -> the fp32 depth map at (2y + dy, 2x + dx)
+    const int q = nw >> 5, dy = q >> 1, dx = q & 1;
+    float hw[FN][4];
     #pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int col = nw + fn * 16 + 4 * g;
-      if (p.R1) r1[fn] = *(const uint2*)(p.R1 + m * p.ldr1 + col);
-      if (p.R2) r2[fn] = *(const uint2*)(p.R2 + m * p.ldr2 + col);
-    }
-  };
-  auto addr = [&](f32x4_t& x, uint2 r) __attribute__((always_inline)) {
-    x[0] += K_::to_f(r.x & 0xffff); x[1] += K_::to_f(r.x >> 16);
-    x[2] += K_::to_f(r.y & 0xffff); x[3] += K_::to_f(r.y >> 16);
-  };
-  loadr(0, r1c, r2c);
-  #pragma unroll
-  for (int fm = 0; fm < FM; ++fm) {
-    if (fm + 1 < FM) loadr(fm + 1, r1n, r2n);
-    #pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      f32x4_t x = acc[fm][fn] + bias[fn];
-      if (p.act == DP_ACT_RELU) {
+    for (int fn = 0; fn < FN; ++fn)
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) hw[fn][r] = p.head_w[(nw & 31) + fn * 16 + 4 * g + r];
+    const long long W2 = 2LL * S;
+    #pragma unroll 1
+    for (int fm = 0; fm < FM; ++fm) {
+      const int y = y0 + wm * 8 + fm, x = x0 + t;
+      float z[FN][4];
+      #pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
         #pragma unroll
-        for (int r = 0; r < 4; ++r) x[r] = fmaxf(x[r], 0.f);
+        for (int r = 0; r < 4; ++r) z[fn][r] = acc[fm][fn][r] + bias[fn][r];
+      const bool top = y == 0 && dy == 0, bot = y == S - 1 && dy == 1;
+      const bool lft = x == 0 && dx == 0, rgt = x == S - 1 && dx == 1;
+      if (top || bot || lft || rgt) {
+        #pragma unroll
+        for (int a = 0; a < 3; ++a)
+          #pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const bool oob = (a == 0 && top) || (a == 2 && bot) || (c == 0 && lft) || (c == 2 && rgt);
+            if (oob) {
+              #pragma unroll
+              for (int fn = 0; fn < FN; ++fn)
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) z[fn][r] -= p.head_corr[(a * 3 + c) * 32 + (nw & 31) + fn * 16 + 4 * g + r];
+            }
+          }
       }
-      if (p.R1) addr(x, r1c[fn]);
-      if (p.R2) addr(x, r2c[fn]);
-      const int chunk = fn * 2 + (g >> 1);
-      uint2 w;
-      w.x = K_::pack2(x[0], x[1]);
-      w.y = K_::pack2(x[2], x[3]);
-      *(uint2*)(slab + t * 128 + ((chunk ^ (t & 7)) << 4) + (g & 1) * 8) = w;
+      // the same per-lane sum order as head_ps_rows over a lane's 8 channels: its 4 (fn = 0) then
+      // its 4 (fn = 1), then the cross-lane sum -- different lanes than the row-raster engine
+      float hs = 0.f;
+      #pragma unroll
+      for (int fn = 0; fn < FN; ++fn)
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) hs += fmaxf(z[fn][r], 0.f) * hw[fn][r];
+      hs += __shfl_xor(hs, 16);
+      hs += __shfl_xor(hs, 32);
+      if (g == 0) ((float*)p.C)[((long long)img * 2 * S + 2 * y + dy) * W2 + 2 * x + dx] = fmaxf(hs + p.head_b, 0.f);
     }
+  } else {
+    // 16-bit rows through the wave's LDS slab (16 rows x TN), stored as whole TN * 2-byte segments
+    constexpr int CH = TN / 8, RPI = 64 / CH;
+    char* slab = smem + wave * (16 * TN * 2);
+    uint2 r1c[FN], r2c[FN], r1n[FN], r2n[FN];
+    auto loadr = [&](int fm, uint2 (&r1)[FN], uint2 (&r2)[FN]) __attribute__((always_inline)) {
+      if constexpr (EPI == CV_EPI_RES) {
+        const long long m = mrow(fm) + t;
+        #pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const int col = nw + fn * 16 + 4 * g;
+          if (p.R1) r1[fn] = *(const uint2*)(p.R1 + m * p.ldr1 + col);
+          if (p.R2) r2[fn] = *(const uint2*)(p.R2 + m * p.ldr2 + col);
+        }
+      }
+    };
+    auto addr = [&](f32x4_t& x, uint2 r) __attribute__((always_inline)) {
+      x[0] += K_::to_f(r.x & 0xffff); x[1] += K_::to_f(r.x >> 16);
+      x[2] += K_::to_f(r.y & 0xffff); x[3] += K_::to_f(r.y >> 16);
+    };
+    loadr(0, r1c, r2c);
     #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int row = k * 8 + (lane >> 3), chunk = lane & 7;
-      const uint4 d = *(const uint4*)(slab + row * 128 + ((chunk ^ (row & 7)) << 4));
-      *(uint4*)((u16*)p.C + (mrow(fm) + row) * p.ldc + nw + chunk * 8) = d;
+    for (int fm = 0; fm < FM; ++fm) {
+      if (fm + 1 < FM) loadr(fm + 1, r1n, r2n);
+      const int y = y0 + wm * 8 + fm, x = x0 + t;
+      const bool border = y == 0 || y == S - 1 || x == 0 || x == S - 1;
+      #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        f32x4_t xv = acc[fm][fn] + bias[fn];
+        if constexpr (EPI == CV_EPI_BC) {
+          // border_correct: the composed conv's bias share of the taps in the next conv's padding
+          if (border) {
+            #pragma unroll 1
+            for (int tp = 0; tp < 9; ++tp) {
+              const int a = tp / 3, c = tp - 3 * (tp / 3);
+              const bool oob = (a == 0 && y == 0) || (a == 2 && y == S - 1) || (c == 0 && x == 0) || (c == 2 && x == S - 1);
+              if (oob) xv -= *(const f32x4_t*)(p.head_corr + tp * p.N + nw + fn * 16 + 4 * g);
+            }
+          }
+        }
+        if (p.act == DP_ACT_RELU) {
+          #pragma unroll
+          for (int r = 0; r < 4; ++r) xv[r] = fmaxf(xv[r], 0.f);
+        }
+        if constexpr (EPI == CV_EPI_RES) {
+          if (p.R1) addr(xv, r1c[fn]);
+          if (p.R2) addr(xv, r2c[fn]);
+        }
+        const int chunk = fn * 2 + (g >> 1);
+        uint2 w;
+        w.x = K_::pack2(xv[0], xv[1]);
+        w.y = K_::pack2(xv[2], xv[3]);
+        *(uint2*)(slab + t * (TN * 2) + ((chunk ^ (t & (CH - 1))) << 4) + (g & 1) * 8) = w;
+      }
+      #pragma unroll
+      for (int k = 0; k < 16 / RPI; ++k) {
+        const int row = k * RPI + lane / CH, chunk = lane % CH;
+        const uint4 d = *(const uint4*)(slab + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4));
+        *(uint4*)((u16*)p.C + (mrow(fm) + row) * p.ldc + nw + chunk * 8) = d;
+      }
+      #pragma unroll
+      for (int fn = 0; fn < FN; ++fn) { r1c[fn] = r1n[fn]; r2c[fn] = r2n[fn]; }
     }
-    #pragma unroll
-    for (int fn = 0; fn < FN; ++fn) { r1c[fn] = r1n[fn]; r2c[fn] = r2n[fn]; }
   }
 }
 
@@ -237,16 +319,34 @@ int launch_cv3(const GemmP& p0, hipStream_t s) {
   GemmP p = p0;
   const int S = p.out_w;
   if (p.k_h != 3 || p.k_w != 3 || p.stride != 1 || p.pad != 1 || p.in_h != S || p.in_w != S || p.out_h != S ||
-      S % CV_T || p.in_c % 64 || p.N % 256 || p.M % (S * S) || p.store_mode != DP_STORE_ROWS || p.row_group ||
-      p.head_w || p.head_corr || p.c_dtype == DP_F32 || p.gamma || p.pos || p.accumulate ||
-      (p.act != DP_ACT_NONE && p.act != DP_ACT_RELU))
+      S % CV_T || p.in_c % 64 || p.M % (S * S) || p.row_group || (p.head_w && p.store_mode != DP_STORE_HEAD_PS) ||
+      p.gamma || p.pos || p.accumulate || (p.act != DP_ACT_NONE && p.act != DP_ACT_RELU))
     return DP_ERR_ARG;
   if ((long long)p.M * p.in_c >= (1LL << 31) || (long long)p.N * p.ldb >= (1LL << 31)) return DP_ERR_ARG;
-  p.tiles_n = p.N / 256;
+  int epi, bn;
+  if (p.store_mode == DP_STORE_HEAD_PS) {
+    if (p.N != 128 || !p.head_w || !p.head_corr || p.c_dtype != DP_F32 || p.R1 || p.R2 || p.act) return DP_ERR_ARG;
+    epi = CV_EPI_HPS; bn = 128;
+  } else if (p.store_mode == DP_STORE_ROWS && p.head_corr) {
+    if (p.c_dtype == DP_F32 || p.R1 || p.R2 || p.N % 128) return DP_ERR_ARG;
+    epi = CV_EPI_BC; bn = p.N % 256 ? 128 : 256;
+  } else if (p.store_mode == DP_STORE_ROWS) {
+    if (p.c_dtype == DP_F32 || p.N % 256) return DP_ERR_ARG;
+    epi = CV_EPI_RES; bn = 256;
+  } else {
+    return DP_ERR_ARG;
+  }
+  p.tiles_n = p.N / bn;
   p.tiles_m = (p.M / (S * S)) * (S / CV_T) * (S / CV_T);
   dim3 grid(p.tiles_m * p.tiles_n);
-  if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true>), grid, dim3(512), 0, s, p);
-  else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false>), grid, dim3(512), 0, s, p);
+#define DP_CV3(B_, E_) do { \
+    if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, B_, E_>), grid, dim3(512), 0, s, p); \
+    else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, B_, E_>), grid, dim3(512), 0, s, p); } while (0)
+  if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);
+  else if (epi == CV_EPI_HPS) DP_CV3(128, CV_EPI_HPS);
+  else if (bn == 256) DP_CV3(256, CV_EPI_BC);
+  else DP_CV3(128, CV_EPI_BC);
+#undef DP_CV3
   DP_CHECK_LAUNCH();
   return 0;
 }

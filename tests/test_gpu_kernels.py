@@ -739,3 +739,56 @@ def test_patch_conv3x3_bit_identical(cuda, dt, case):
     torch.cuda.synchronize()
     assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max().item()
     close(out1.reshape(nb, S, S, Co).permute(0, 3, 1, 2), ref, dt, f"cv3 {case}")
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_patch_conv3x3_head_epilogues(cuda, dt):
+    """The patch-conv engine's head convs (128 output channels per tile): the border-corrected
+    composed conv (out_conv∘head.0) bit-identical to the 512 x 128 engine, and the composed depth
+    head (HEAD_PS: deconv∘3x3∘ReLU∘1x1∘ReLU, one parity per wave) equal to it up to the order of
+    the 32-channel dot product; both against the reference layer order in fp32."""
+    from depth_pro._lib import DP_TILE_CV3_256x256
+    from depth_pro.engine import compose_head, compose_head0
+
+    g = torch.Generator().manual_seed(43)
+    S, c, o = 96, 256, 128
+    y = torch.randn(1, c, S, S, generator=g)
+    wo = torch.randn(c, c, generator=g) * c ** -0.5
+    bo = torch.randn(c, generator=g)
+    w0 = torch.randn(o, c, 3, 3, generator=g) * (9 * c) ** -0.5
+    b0 = torch.randn(o, generator=g)
+    yq = y.to(dt).float()
+    ref = F.conv2d(F.conv2d(yq, wo[:, :, None, None], bo), w0, b0, padding=1)[0].permute(1, 2, 0).reshape(S * S, o)
+    P = {k: v.to(cuda) for k, v in compose_head0(w0, b0, wo, bo, dt).items()}
+    x = yq[0].permute(1, 2, 0).reshape(S * S, c).contiguous().to(dt).to(cuda)
+    kw = dict(M=S * S, N=o, K=9 * c, conv=dict(in_h=S, in_w=S, in_c=c, k=3, stride=1, pad=1, out_h=S, out_w=S),
+              bias=P["head.0c.b"], border_corr=P["head.0c.corr"])
+    out1 = torch.full((S * S, o), float("nan"), dtype=dt, device=cuda)
+    out2 = out1.clone()
+    ops.gemm(x, P["head.0c.w"], out1, tile=DP_TILE_CV3_256x256, **kw)
+    ops.gemm(x, P["head.0c.w"], out2, tile=DP_TILE_BIG_512x128, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max().item()
+    close(out1, ref, dt, "cv3 border-corrected composed conv")
+
+    ci, H = 128, 48
+    h0 = torch.randn(1, ci, H, H, generator=g).to(dt).float()
+    wd = torch.randn(ci, ci, 2, 2, generator=g) * ci ** -0.5
+    bd = torch.randn(ci, generator=g)
+    w2 = torch.randn(32, ci, 3, 3, generator=g) * (9 * ci) ** -0.5
+    b2 = torch.randn(32, generator=g)
+    w4 = torch.randn(32, generator=g) * 32 ** -0.5
+    Q = {k: (v.to(cuda) if torch.is_tensor(v) else v) for k, v in compose_head(wd, bd, w2, b2, dt).items()}
+    xh = h0[0].permute(1, 2, 0).reshape(H * H, ci).contiguous().to(dt).to(cuda)
+    kh = dict(M=H * H, N=128, K=9 * ci, conv=dict(in_h=H, in_w=H, in_c=ci, k=3, stride=1, pad=1, out_h=H, out_w=H),
+              bias=Q["head.ps.b"], head_w=w4.to(cuda), head_b=0.25, head_corr=Q["head.ps.corr"])
+    d1 = torch.full((2 * H, 2 * H), float("nan"), device=cuda)
+    d2 = d1.clone()
+    ops.gemm(xh, Q["head.ps.w"], d1, tile=DP_TILE_CV3_256x256, **kh)
+    ops.gemm(xh, Q["head.ps.w"], d2, tile=DP_TILE_BIG_512x128, **kh)
+    torch.cuda.synchronize()
+    assert not torch.isnan(d1).any()
+    assert (d1 - d2).abs().max().item() <= 1e-5 * (d2.abs().max().item() + 1e-6)
+    r = F.conv_transpose2d(h0, wd, bd, stride=2)
+    r = F.relu(F.conv2d(F.relu(F.conv2d(r, w2, b2, padding=1)), w4.reshape(1, 32, 1, 1), torch.tensor([0.25])))
+    close(d1, r[0, 0], dt, "cv3 head HEAD_PS")
