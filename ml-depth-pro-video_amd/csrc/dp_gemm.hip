@@ -111,11 +111,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   tile = a->tile;
   if (a->store_mode == DP_STORE_HEAD_PS) {
     // 32-column parity groups must not straddle a wave's columns (TN = 32 or 64); the patch-conv
-    // engine (one parity per wave) when asked for, or for maps it tiles (A/B: debug 4096 = off)
-    const bool cv3 = a->in_w % 16 == 0 && a->in_h == a->in_w && a->M >= 512 * 256 && a->in_c % 64 == 0 &&
-                     a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 && !(dbg & 4096);
-    if (tile == DP_TILE_AUTO && cv3) tile = DP_TILE_CV3_256x256;
-    else if (tile != DP_TILE_CV3_256x256) tile = a->M >= 512 * 256 ? DP_TILE_BIG_512x128 : DP_TILE_BIG_256x128;
+    // engine (one parity per wave) only when asked for: at 768^2 it runs 347 - 355 us in-frame vs
+    // 249 - 255 on the 512 x 128 engine (profiles/r03w/)
+    if (tile != DP_TILE_CV3_256x256) tile = a->M >= 512 * 256 ? DP_TILE_BIG_512x128 : DP_TILE_BIG_256x128;
   } else if (a->head_w) {
     if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;
     tile = DP_TILE_256x32;

@@ -106,15 +106,16 @@ def test_gemm_plan_tile_choice():
     assert conv(768, 256, **wsk)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
     assert conv(384, 256, **wsk)[1] != _lib.DP_TILE_CV3_256x256
     # the head convs at 768^2 (128 output channels): the composed out_conv∘head.0 with its border
-    # correction and the composed depth head (HEAD_PS) on the patch-conv engine; debug 4096 keeps
-    # them on the 512 x 128 engine
+    # correction on the patch-conv engine (debug 4096: the 512 x 128 engine); the composed depth
+    # head (HEAD_PS) on the 512 x 128 engine unless the patch-conv engine is asked for
     def head(**kw):
         return plan(768 * 768, 128, 9 * kw.pop("cin"), a_mode=_lib.DP_A_CONV, in_h=768, in_w=768, k_h=3, k_w=3,
                     stride=1, pad=1, out_h=768, out_w=768, head_corr=256, **kw)
     h0c = dict(cin=256, in_c=256)
     hps = dict(cin=128, in_c=128, store_mode=_lib.DP_STORE_HEAD_PS, head_w=256, c_dtype=_lib.DP_F32)
     assert head(**h0c)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
-    assert head(**hps)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
+    assert head(**hps)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)
+    assert head(**hps, tile=_lib.DP_TILE_CV3_256x256)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
     lib.dp_gemm_debug_flags(4096)
     try:
         assert head(**h0c)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)
