@@ -706,17 +706,21 @@ def test_8phase_320_bit_identical_to_320(cuda, dt, case):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("case", ["relu_bias_relu", "residual2", "cin128_n512"])
+@pytest.mark.parametrize("case", ["relu_bias_relu", "residual2", "cin128_n512",
+                                  "big_relu_bias_relu", "big_residual2_cin192", "big_cin128_n512"])
 def test_patch_conv3x3_bit_identical(cuda, dt, case):
     """The 3x3 patch-conv engine (DP_TILE_CV3_256x256: 16 x 16 pixel tiles, the input patch of a
     channel block in LDS, the 9 taps read from it) gives exactly the 256 x 256 big engine's result
     -- same K order, same zero padding, same epilogue -- for the decoder ResidualBlock convs (ReLU
-    on load + bias + ReLU; bias + two residuals), 2 images, a wider N; and matches F.conv2d."""
+    on load + bias + ReLU; bias + two residuals), 2 images, a wider N; and matches F.conv2d.
+    big_*: more tiles than CUs (576 tiles; 2 x 256 tiles with 3 channel blocks = an odd K-step count
+    per tile; 2 column tiles of 144)."""
     from depth_pro._lib import DP_TILE_CV3_256x256
 
     g = torch.Generator().manual_seed(sum(map(ord, case)))
     S, Ci, Co, nb = {"relu_bias_relu": (96, 256, 256, 1), "residual2": (64, 256, 256, 2),
-                     "cin128_n512": (48, 128, 512, 1)}[case]
+                     "cin128_n512": (48, 128, 512, 1), "big_relu_bias_relu": (384, 256, 256, 1),
+                     "big_residual2_cin192": (256, 192, 256, 2), "big_cin128_n512": (192, 128, 512, 1)}[case]
     x = rnd(nb, Ci, S, S, dt=dt, dev=cuda, gen=g)
     w = rnd(Co, Ci, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * Ci) ** -0.5)
     b = torch.randn(Co, generator=g).to(cuda)
@@ -724,10 +728,10 @@ def test_patch_conv3x3_bit_identical(cuda, dt, case):
     kw = dict(M=nb * S * S, N=Co, K=9 * Ci, conv=dict(in_h=S, in_w=S, in_c=Ci, k=3, stride=1, pad=1, out_h=S, out_w=S),
               bias=b)
     ref = F.conv2d(x.float(), w.float(), b, padding=1)
-    if case == "relu_bias_relu":
+    if case.endswith("relu_bias_relu"):
         kw.update(relu_a=True, act=DP_ACT_RELU)
         ref = F.relu(F.conv2d(F.relu(x.float()), w.float(), b, padding=1))
-    elif case == "residual2":
+    elif "residual2" in case:
         r1 = rnd(nb * S * S, Co, dt=dt, dev=cuda, gen=g)
         r2 = rnd(nb * S * S, Co, dt=dt, dev=cuda, gen=g)
         kw.update(R1=r1, ldr1=Co, R2=r2, ldr2=Co)
