@@ -112,10 +112,10 @@ typedef struct dp_gemm_args {
   const float* head_w;      /* [N] or NULL */
   float head_b;
   const float* head_corr;   /* DP_STORE_HEAD_PS: [9][32] border corrections; DP_STORE_ROWS with a
-                               stride-1 pad-1 3x3 implicit conv on the 512x128 engine (N = 128 at
-                               M >= 512*256, or that tile hint): [9][N] per-tap values
-                               subtracted where the tap falls in the zero padding (a composed
-                               1x1-then-3x3 conv's bias); else NULL */
+                               stride-1 pad-1 3x3 implicit conv on the 512x128 or the patch-conv
+                               engine (N = 128 at M >= 512*256, or those tile hints): [9][N]
+                               per-tap values subtracted where the tap falls in the zero padding
+                               (a composed 1x1-then-3x3 conv's bias); else NULL */
   int32_t tile;             /* 0 = auto, else a DP_TILE_* hint */
   void* workspace;          /* NULL, or >= dp_gemm_workspace_size() bytes of device memory owned by
                                the caller for THIS stream (never shared by concurrent launches);
@@ -136,7 +136,9 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
    ReLU prologue, N % 256 == 0; 16-bit C without per-row operands, or an fp32 C accumulated into
    without activation); the auto choice for the ViT qkv / proj / fc2.  A hint an engine cannot
    serve returns DP_ERR_ARG.  DP_TILE_CV3_256x256: stride-1 pad-1 3x3 implicit conv on 16 x 16 pixel
-   tiles with the input patch in LDS (square maps, side % 16 == 0, in_c % 64 == 0, N % 256 == 0). */
+   tiles with the input patch in LDS (square maps, side % 16 == 0, in_c % 64 == 0; N % 256 == 0 with
+   ReLU / residual epilogues, or N % 128 == 0 with head_corr, or DP_STORE_HEAD_PS); the auto choice
+   for the many-round ResidualBlock convs and the border-corrected composed conv at 768^2. */
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 
