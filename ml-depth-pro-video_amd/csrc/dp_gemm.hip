@@ -185,9 +185,16 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     const long long ext = (last * a->ldc + a->N) * (a->c_dtype == DP_F32 ? 4 : 2);
     if (ext < 0xFFFFFF00LL) c_bytes = (unsigned)ext;
   }
+  // the same for the deconv store of the persistent 8-phase engine (4 M output pixels; no other
+  // engine takes c_bytes with that store mode)
+  unsigned dcv_bytes = 0;
+  if (a->store_mode == DP_STORE_DECONV2X2 && a->c_dtype != DP_F32) {
+    const long long ext = ((4LL * a->M - 1) * a->ldc + a->dc_cout) * 2;
+    if (ext < 0xFFFFFF00LL) dcv_bytes = (unsigned)ext;
+  }
   // the persistent engine keeps 32-bit operand offsets
-  if (a->a_mode == DP_A_DENSE && (long long)a->M * a->lda >= (1LL << 31)) c_bytes = 0;
-  if ((long long)a->N * a->ldb >= (1LL << 31)) c_bytes = 0;
+  if (a->a_mode == DP_A_DENSE && (long long)a->M * a->lda >= (1LL << 31)) c_bytes = dcv_bytes = 0;
+  if ((long long)a->N * a->ldb >= (1LL << 31)) c_bytes = dcv_bytes = 0;
   if ((tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) && (!c_bytes || a->N % 256)) return DP_ERR_ARG;
   // Multi-round GEMMs on the 320 x 256 / 256 x 256 engines (the ViT qkv: 768 tiles, the
   // 768^2 decoder convs: 2304) run persistent: the next tile's first K step loads under
@@ -208,12 +215,19 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // (in-frame A/B, profiles/r03c_p8ph, r03d: 46.67 -> 46.79 / 46.95 fps; debug 1 << 22: off)
   // (measured and rejected: an implicit-conv A loader for the 768^2 ResidualBlock convs, 675 vs
   // 666 us on the persistent big engine, profiles/r03g_conv768_p8ph.txt)
+  // the 2x2 stride-2 deconvs with many tiles (the decoder's 192^2 -> 384^2 and 384^2 -> 768^2 ones)
+  // on it too: short K (4 steps per tile), so the epilogue stores bound them, and here they drain
+  // under the next tile's K loop: 162 - 166 -> 136 - 137 and 62 -> 47 us in-frame, 47.93 / 48.09
+  // -> 48.28 / 48.37 fps (profiles/r03ab_deconv_p8ph/; debug 1 << 23: off)
+  const bool dcv = a->store_mode == DP_STORE_DECONV2X2 && !a->relu_a && !a->gamma && a->act == DP_ACT_NONE;
+  if (a->tile == DP_TILE_AUTO && dcv && !(dbg & (1 << 23)) && tiles256 >= 2LL * num_cus()) tile = DP_TILE_P8PH_256x256;
   if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && !(dbg & (1 << 22)))) {
-    const bool ok = a->a_mode == DP_A_DENSE && a->N % 256 == 0 && a->K >= 128 && c_bytes && a->c_dtype != DP_F32 &&
-                    a->store_mode == DP_STORE_ROWS && !a->R1 && !a->R2 && !a->pos && !a->accumulate &&
+    const bool ok = a->a_mode == DP_A_DENSE && a->N % 256 == 0 && a->K >= 128 && a->c_dtype != DP_F32 &&
+                    ((a->store_mode == DP_STORE_ROWS && c_bytes) || (dcv && dcv_bytes)) && !a->R1 && !a->R2 && !a->pos && !a->accumulate &&
                     !a->row_group && !a->head_w && !a->head_corr && !(dbg & (1 << 20));
     if (tile == DP_TILE_P8PH_256x256 && !ok) return DP_ERR_ARG;
     if (ok) tile = DP_TILE_P8PH_256x256;
+    if (ok && dcv) c_bytes = dcv_bytes;
   }
   // the 8-phase 320 x 256 engine: dense, no ReLU prologue, N % 256 == 0, and an epilogue it has
   // (load-free with a 16-bit C, or the fp32 residual accumulate without activation) -- the

@@ -1637,7 +1637,7 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
 // (filled by LDS-DMA with the tile's loads), so the epilogue issues no global load: hipcc
 // would put a vmcnt(0) in front of one -- a wait for every LDS-DMA in flight, i.e. the next
 // tile's first K steps.
-template <typename K_, int ACT, bool HG>
+template <typename K_, int ACT, bool HG, bool DCV>
 __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)[8][4], char* slab,
                                                   const float* cst, int lane, int m_base, int n_base,
                                                   __amdgpu_buffer_rsrc_t crs) {
@@ -1677,13 +1677,27 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
       const int row = k * RPI + lane / CH, chunk = lane % CH;
       const uint4 d = *(const uint4*)(slab + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4));
       const int m = m_base + f0 * 16 + row, n = n_base + chunk * 8;
-      const unsigned bo = (m < p.M && n < p.N) ? (unsigned)(((long long)m * p.ldc + n) * 2) : p.c_bytes;
+      unsigned bo = p.c_bytes;
+      if (m < p.M && n < p.N) {
+        if constexpr (DCV) {
+          // DP_STORE_DECONV2X2 (epilogue4): row m = input pixel (b, y, x), column n = sub-pixel q,
+          // channel co -> output pixel (b, 2y + q / 2, 2x + q % 2)
+          const int hw = p.dc_h * p.dc_w;
+          const int b = m / hw, rr = m - b * hw;
+          const int y = rr / p.dc_w, x = rr - y * p.dc_w;
+          const int q = n / p.dc_cout, co = n - q * p.dc_cout;
+          const long long pix = ((long long)b * 2 * p.dc_h + 2 * y + (q >> 1)) * (2 * p.dc_w) + 2 * x + (q & 1);
+          bo = (unsigned)((pix * p.ldc + co) * 2);
+        } else {
+          bo = (unsigned)(((long long)m * p.ldc + n) * 2);
+        }
+      }
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{d.x, d.y, d.z, d.w}, crs, bo, 0, 0);
     }
   }
 }
 
-template <typename K_, bool RELU, int ACT, bool HG>
+template <typename K_, bool RELU, int ACT, bool HG, bool DCV = false>
 __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
   constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
@@ -1877,7 +1891,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     int tm, tn;
     tile_coords(p, t_cur, tm, tn);
     const float* cst = (const float*)(smem + RING + 8 * SLAB + (wave * 2 + (i & 1)) * CST);
-    epilogue_mfma_buf<K_, ACT, HG>(p, acc, slab, cst, lane, tm * 256 + wm * TM, tn * 256 + wn * TN, crs);
+    epilogue_mfma_buf<K_, ACT, HG, DCV>(p, acc, slab, cst, lane, tm * 256 + wm * TM, tn * 256 + wn * TN, crs);
     if (t_nxt < 0) break;
     t_cur = t_nxt;
     t_nxt = next_tile(t_cur);
@@ -1891,11 +1905,21 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
   p.tiles_n = p.N / 256;
   p.tiles_m = (p.M + 255) / 256;
   const int T = p.tiles_n * p.tiles_m;
-  const int ea = fast_epi_act(p);
+  const bool dcv = p.store_mode == DP_STORE_DECONV2X2;
+  const int ea = dcv ? p.act : fast_epi_act(p);
   if (p.N % 256 || p.K < 128 || !p.c_bytes || p.c_dtype == DP_F32 || ea < 0 || ea >= EPI_ACC) return DP_ERR_ARG;
   int G = num_cus();
   if (G > T) G = T;
   dim3 grid(G);
+  if (dcv) {   // the 2x2 stride-2 deconvs: bias only (no per-row operands, no activation)
+    if (p.relu_a || p.gamma || p.pos || p.R1 || p.R2 || p.accumulate || p.row_group || p.head_w || p.head_corr ||
+        ea != DP_ACT_NONE || p.dc_cout % 8 || p.dbg & (1 << 20))
+      return DP_ERR_ARG;
+    hipLaunchKernelGGL((gemm_p8ph_kernel<K_, false, DP_ACT_NONE, false, true>), grid, dim3(512), 0, s, p);
+    DP_CHECK_LAUNCH();
+    return 0;
+  }
+  if (p.store_mode != DP_STORE_ROWS) return DP_ERR_ARG;
 #define DP_P8(R_, G_) do { \
     if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_NONE, G_>), grid, dim3(512), 0, s, p); \
     else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_RELU, G_>), grid, dim3(512), 0, s, p); \

@@ -123,6 +123,40 @@ def test_deconv2x2_pixel_shuffle_store(cuda, dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("case", ["s96_c256_bias", "s40_c512_cat_nobias", "b2_s64_c256"])
+def test_deconv2x2_persistent_8phase_bit_identical(cuda, dt, case):
+    """The persistent 8-phase engine with the 2x2 stride-2 deconv store (output pixel (2y + q/2,
+    2x + q%2) per GEMM row and column group q): bit-identical to the 256 x 256 engine -- into a
+    concat buffer's second half, without bias, ragged last row tile, 2 images -- and vs
+    F.conv_transpose2d."""
+    from depth_pro._lib import DP_TILE_P8PH_256x256
+
+    g = torch.Generator().manual_seed(sum(map(ord, case)))
+    S, cin, cout, nb, bias, cat = {"s96_c256_bias": (96, 256, 256, 1, True, False),
+                                   "s40_c512_cat_nobias": (40, 512, 256, 1, False, True),
+                                   "b2_s64_c256": (64, 256, 256, 2, True, False)}[case]
+    x = rnd(nb, cin, S, S, dt=dt, dev=cuda, gen=g)
+    w = rnd(cin, cout, 2, 2, dt=dt, dev=cuda, gen=g, scale=cin ** -0.5)
+    b = torch.randn(cout, generator=g).to(cuda) if bias else None
+    xh = x.permute(0, 2, 3, 1).reshape(nb * S * S, cin).contiguous()
+    wp = w.permute(2, 3, 1, 0).reshape(4 * cout, cin).contiguous()
+    ldc = 2 * cout if cat else cout
+    kw = dict(M=nb * S * S, N=4 * cout, K=cin, bias=b.repeat(4) if bias else None, deconv=(S, S, cout),
+              C_off=cout if cat else 0, ldc=ldc)
+    out1 = torch.full((nb * 4 * S * S, ldc), 3.0, dtype=dt, device=cuda)
+    out2 = out1.clone()
+    ops.gemm(xh, wp, out1, tile=DP_TILE_P8PH_256x256, **kw)
+    ops.gemm(xh, wp, out2, tile=DP_TILE_BIG_256x256, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max().item()
+    ref = F.conv_transpose2d(x.float(), w.float(), b, stride=2)
+    got = out1[:, ldc - cout:].reshape(nb, 2 * S, 2 * S, cout).permute(0, 3, 1, 2)
+    close(got, ref, dt, f"p8ph deconv {case}")
+    if cat:
+        assert (out1[:, :cout] == 3.0).all()
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 def test_head_conv_with_fused_1x1(cuda, dt):
     g = torch.Generator().manual_seed(13)
     S, cin = 40, 128
