@@ -215,12 +215,15 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // (in-frame A/B, profiles/r03c_p8ph, r03d: 46.67 -> 46.79 / 46.95 fps; debug 1 << 22: off)
   // (measured and rejected: an implicit-conv A loader for the 768^2 ResidualBlock convs, 675 vs
   // 666 us on the persistent big engine, profiles/r03g_conv768_p8ph.txt)
-  // the 2x2 stride-2 deconvs with many tiles (the decoder's 192^2 -> 384^2 and 384^2 -> 768^2 ones)
-  // on it too: short K (4 steps per tile), so the epilogue stores bound them, and here they drain
-  // under the next tile's K loop: 162 - 166 -> 136 - 137 and 62 -> 47 us in-frame, 47.93 / 48.09
-  // -> 48.28 / 48.37 fps (profiles/r03ab_deconv_p8ph/; debug 1 << 23: off)
+  // the 2x2 stride-2 deconvs with >= 128 tiles on it too: short K (4 steps per tile at K = 256),
+  // so the epilogue stores bound them, and here they drain under the next tile's K loop (or go
+  // out as buffer stores from the MFMA layout): 384^2 -> 768^2 162 - 166 -> 136 - 137, 192^2 ->
+  // 384^2 62 -> 47 us in-frame, 47.93 / 48.09 -> 48.28 / 48.37 fps (profiles/r03ab_deconv_p8ph/);
+  // 96^2 -> 192^2 29.6 -> 22, 48^2 -> 96^2 (K = 1024) 42.7 -> 36, 96^2 (N = 2048) 47.5 -> 44.6 us;
+  // 48 and 36 tiles were slower (26.9 -> 34, 17.1 -> 18.3 us; profiles/r03ad_deconv_small/).
+  // Debug 1 << 23: off.
   const bool dcv = a->store_mode == DP_STORE_DECONV2X2 && !a->relu_a && !a->gamma && a->act == DP_ACT_NONE;
-  if (a->tile == DP_TILE_AUTO && dcv && !(dbg & (1 << 23)) && tiles256 >= 2LL * num_cus()) tile = DP_TILE_P8PH_256x256;
+  if (a->tile == DP_TILE_AUTO && dcv && !(dbg & (1 << 23)) && tiles256 >= 128) tile = DP_TILE_P8PH_256x256;
   if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && !(dbg & (1 << 22)))) {
     const bool ok = a->a_mode == DP_A_DENSE && a->N % 256 == 0 && a->K >= 128 && a->c_dtype != DP_F32 &&
                     ((a->store_mode == DP_STORE_ROWS && c_bytes) || (dcv && dcv_bytes)) && !a->R1 && !a->R2 && !a->pos && !a->accumulate &&

@@ -116,14 +116,16 @@ def test_gemm_plan_tile_choice():
     assert head(**h0c)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
     assert head(**hps)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)
     assert head(**hps, tile=_lib.DP_TILE_CV3_256x256)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
-    # the decoder's many-tile 2x2 deconvs (384^2 -> 768^2, 192^2 -> 384^2): the persistent 8-phase
-    # engine with the pixel-shuffle store; fewer tiles stay where they were
+    # the decoder's 2x2 deconvs with >= 128 tiles of 256 x 256: the persistent 8-phase engine with
+    # the pixel-shuffle store; fewer tiles stay where they were
     def deconv(S, cin, cout, **kw):
         return plan(S * S, 4 * cout, cin, store_mode=_lib.DP_STORE_DECONV2X2, dc_h=S, dc_w=S, dc_cout=cout,
                     ldc=cout, dtype=_lib.DP_F16, c_dtype=_lib.DP_F16, bias=256, **kw)
     assert deconv(384, 256, 256, **wsk)[1:] == (_lib.DP_TILE_P8PH_256x256, 256)
     assert deconv(192, 256, 256, **wsk)[1:] == (_lib.DP_TILE_P8PH_256x256, 256)
-    assert deconv(96, 512, 512, **wsk)[1] != _lib.DP_TILE_P8PH_256x256
+    assert deconv(96, 512, 512, **wsk)[1:] == (_lib.DP_TILE_P8PH_256x256, 256)     # 288 tiles
+    assert deconv(96, 256, 256, **wsk)[1:] == (_lib.DP_TILE_P8PH_256x256, 144)     # 144 tiles, one round
+    assert deconv(48, 256, 256, **wsk)[1] != _lib.DP_TILE_P8PH_256x256             # 36 tiles
     assert deconv(384, 256, 256, act=_lib.DP_ACT_RELU, **wsk)[1] != _lib.DP_TILE_P8PH_256x256
     lib.dp_gemm_debug_flags(4096)
     try:
