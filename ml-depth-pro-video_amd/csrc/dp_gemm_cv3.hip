@@ -167,6 +167,22 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     const int pb = cb & 1, st = t & 1;
     const bool np = tap == 0 && cb + 1 < CB;    // this step streams the next block's patch
     const bool n2 = t + 2 < KT;
+    if constexpr (BN == 128) {
+      // 128-channel tiles: two half-step phases of 16 MFMAs (A rows qm, both column halves) --
+      // four phases of 8 spent most of the step at barriers.  Phase 0 reads the step's weights
+      // and streams the next block's patch (its buffer was last read one phase earlier by the
+      // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
+      // phase 0) and waits for step t+1.
+      readA(0, pb, ky, kx); readB(0, st); readB(1, st);
+      if (np) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
+      bar(); mma(0, 0); mma(0, 1); bar();
+      readA(1, pb, ky, kx);
+      if (n2) issue_b(0, t + 2);
+      if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
+      else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
+      bar(); mma(1, 0); mma(1, 1); bar();
+      continue;
+    }
     // phase 0: quadrant (0,0)
     readA(0, pb, ky, kx); readB(0, st);
     if (np) issue_patch3(cb + 1, pb ^ 1, 0);
