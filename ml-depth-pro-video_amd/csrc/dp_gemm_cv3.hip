@@ -12,9 +12,10 @@
 // pixels; K order (channel block, tap, 64 channels) = the packed conv weights
 // ([Cout][Cin/64][ky][kx][64], ops.conv_weight).  LDS: 2 patch buffers (48 LDS-DMA pieces of
 // 1 KiB each: 324 pixels x 128 B, the 16-B chunk XOR-swizzled by pixel index, 7 dummy pieces
-// so every wave issues 6) + a 2-stage ring of weight K steps = 160 KiB.  The K loop is the
-// 8-phase schedule of gemm_8ph_kernel (two wave groups staggered by one barrier, one LDS-DMA
-// group per phase, one counted wait per step) with the A fragments read from the patch.  The
+// so every wave issues 6) + a 2-stage ring of weight K steps = 160 KiB.  The K loop: two
+// half-step phases per K step (two wave groups staggered by one barrier, LDS-DMA issued in the
+// phase after its buffer's last read, one counted wait per step) with the A fragments read from
+// the patch.  The
 // epilogue (bias, ReLU, residuals R1 / R2, 16-bit C) works in the MFMA register layout, one
 // 16-pixel output row segment per fragment row.
 #include "dp_gemm_impl.h"
@@ -143,12 +144,10 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   };
   auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
 
-  // The 8-phase schedule of gemm_8ph_kernel, A from the patch: per K step (channel block cb,
-  // tap) four quadrant phases {fragment reads, LDS-DMA, s_barrier, 16 MFMAs, s_barrier}; reads
-  // p0 A(qm0) + B(qn0), p1 B(qn1), p2 A(qm1); weight halves of step t+2 in phases 2 / 3 (their
-  // stage's weight reads ended in phase 1), the next block's patch in phases 0 / 1 of a block's
-  // first step (its buffer was last read two phases earlier); wave rows staggered by a barrier;
-  // one counted wait per step (phase 3) for step t+1.
+  // K loop: per K step (channel block cb, tap) two half-step phases {fragment reads, LDS-DMA,
+  // s_barrier, MFMAs, s_barrier}; wave rows staggered by a barrier; weight step t+2 streamed in
+  // phase 1 (its stage's reads ended in phase 0), the next block's patch in phase 0 of a block's
+  // first step; one counted wait per step (phase 1) for step t+1.
   // prologue: patch of block 0 and weight steps 0 and 1
   issue_patch3(0, 0, 0); issue_patch3(0, 0, 3);
   #pragma unroll
@@ -167,42 +166,22 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     const int pb = cb & 1, st = t & 1;
     const bool np = tap == 0 && cb + 1 < CB;    // this step streams the next block's patch
     const bool n2 = t + 2 < KT;
-    if constexpr (BN == 128) {
-      // 128-channel tiles: two half-step phases of 16 MFMAs (A rows qm, both column halves) --
-      // four phases of 8 spent most of the step at barriers.  Phase 0 reads the step's weights
-      // and streams the next block's patch (its buffer was last read one phase earlier by the
-      // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
-      // phase 0) and waits for step t+1.
-      readA(0, pb, ky, kx); readB(0, st); readB(1, st);
-      if (np) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
-      bar(); mma(0, 0); mma(0, 1); bar();
-      readA(1, pb, ky, kx);
-      if (n2) issue_b(0, t + 2);
-      if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
-      else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
-      bar(); mma(1, 0); mma(1, 1); bar();
-      continue;
-    }
-    // phase 0: quadrant (0,0)
-    readA(0, pb, ky, kx); readB(0, st);
-    if (np) issue_patch3(cb + 1, pb ^ 1, 0);
-    bar(); mma(0, 0); bar();
-    // phase 1: quadrant (0,1)
-    readB(1, st);
-    if (np) issue_patch3(cb + 1, pb ^ 1, 3);
-    bar(); mma(0, 1); bar();
-    // phase 2: quadrant (1,0)
+    // two half-step phases (A rows qm, both column halves: 16 MFMAs per wave at BN 128, 32 at
+    // BN 256) instead of four quadrant phases -- half the barriers per step (head.0c 449 / 453
+    // -> 433 / 421 us, the 768^2 ResidualBlock convs 676 / 684 -> 642 / 629 us in-frame,
+    // profiles/r03af_cv3_bn128_2phase/, r03ag_cv3_2phase/).  Phase 0 reads the step's weights
+    // and streams the next block's patch (its buffer was last read one phase earlier by the
+    // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
+    // phase 0), waits for step t+1, then issues the second weight half.
+    readA(0, pb, ky, kx); readB(0, st); readB(1, st);
+    if (np) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
+    bar(); mma(0, 0); mma(0, 1); bar();
     readA(1, pb, ky, kx);
     if (n2) issue_b(0, t + 2);
-    bar(); mma(1, 0); bar();
-    // phase 3: quadrant (1,1); weight step t+1 (and a next block's patch) landed before this
-    // phase's first barrier -- younger: this step's patch pieces and the first half of step t+2
-    // (BN 128: its only half)
     if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
     else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
-    if (NBH == 2 && n2) issue_b(NBH - 1, t + 2);
-    bar(); mma(1, 1);
-    bar();
+    if (NBH == 2 && n2) issue_b(1, t + 2);
+    bar(); mma(1, 0); mma(1, 1); bar();
   }
   if (wm == 0) bar();
 
