@@ -68,6 +68,28 @@ def pmc_traffic(kernel: str, workgroups: int):
     return None
 
 
+# The rocprofv3 --kernel-trace --stats summary of this tree's bench run (tools/gpu_check.sh prof,
+# copied from gpurun_out/): the dominant kernel's average duration there is reported beside the live
+# HIP-event figure, so the line's roofline fraction can be checked against the committed profile.
+PROF_STATS = "profiles/r04_kernel_stats.csv"
+
+
+def rocprof_avg_us(kernel: str):
+    """(average us, calls) of the kernels whose name starts with `kernel` in PROF_STATS, or None."""
+    import csv
+    path = os.path.join(REPO, PROF_STATS)
+    try:
+        rows = list(csv.DictReader(open(path)))
+    except OSError:
+        return None
+    hit = [r for r in rows if r["Name"].startswith("void " + kernel) or r["Name"].startswith(kernel)]
+    if not hit:
+        return None
+    calls = sum(int(r["Calls"]) for r in hit)
+    ns = sum(float(r["TotalDurationNs"]) for r in hit)
+    return ns / calls / 1e3, calls
+
+
 def frame(seed: int) -> np.ndarray:
     return np.random.default_rng(seed=seed).integers(0, 256, (1536, 1536, 3), dtype=np.uint8)
 
@@ -137,6 +159,32 @@ def cpu_baseline() -> dict:
                       f"after a 1-block warm-up), {dt:.1f} s"}
 
 
+def refuse(msg: str, code: int) -> None:
+    """Exit non-zero WITHOUT a bench line: a number from such a run would be meaningless."""
+    print(json.dumps({"error": msg, "value": None}), flush=True)
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def launch_ranks(n: int) -> None:
+    """`python bench.py --gpus N` (N > 1) outside a torch.distributed launcher: start the N ranks
+    here, one process per GPU (torch.distributed.run, rendezvous on 127.0.0.1), before this process
+    makes any GPU call, and exit with the launcher's status.  Fails (non-zero) when fewer than N
+    devices are visible, so the line can never report fewer GPUs than requested."""
+    import socket
+    import subprocess
+
+    ndev = torch.cuda.device_count()       # counts devices without initialising HIP
+    if ndev < n:
+        refuse(f"--gpus {n} requested but only {ndev} GPU(s) are visible", 2)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,9 +196,21 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct resident frames per rank")
+    ap.add_argument("--ab", action="store_true",
+                    help="A/B timing run (tools/ab_bench.sh): allows DP_GEMM_DEBUG / DP_ABLATE and reports "
+                         "'ab_fps' instead of a bench 'value'")
     args = ap.parse_args()
 
+    # a run whose results are wrong by construction (ablations) or whose schedule is not the product's
+    # (debug switches) prints no value
+    forced = [v for v in ("DP_ABLATE", "DP_GEMM_DEBUG", "DP_ATTN_DEBUG") if os.environ.get(v, "") not in ("", "0")]
+    if forced and not args.ab:
+        refuse(f"{', '.join(forced)} set: ablation / debug switches make the frame invalid (use --ab)", 3)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        refuse(f"--gpus {args.gpus} but the launcher started {world} rank(s)", 2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -191,6 +251,7 @@ def main():
     pending = [None, None]
 
     counter = [0]
+    statuses = []          # FrameStatus of every frame this rank ran (checked after the timed loop)
 
     def step(i):
         d = depths[i & 1]
@@ -204,7 +265,7 @@ def main():
         ops.normalize_u8(frames[n % len(frames)], eng.x0)
         c, fov = eng.run()
         ops.infer_epilogue(c, fov, None, 1536, 1536, d, fpx, eng.status_dev[-1:])
-        eng.finish_status()
+        statuses.append(eng.finish_status())
         if world > 1:
             _, pending[i & 1] = D.gather_frames(d, dst=0, async_op=True)
 
@@ -239,18 +300,24 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     fps_per_gpu = fps / world
 
-    # per-kernel roofline leg: one instrumented eager frame (side encoders serialised onto
-    # the main stream so no launch overlaps another), HIP events on the launching stream
-    # around every launch; grouped by (kernel kind, shape)
+    # every benched frame healthy: no timed-out stream-K hand-off, depth / focal length all finite
+    bad = [st for st in statuses if st.error() is not None]
+    if bad and not args.ab:
+        refuse(f"rank {rank}: {len(bad)} of {len(statuses)} benched frames invalid "
+               f"(first: frame {bad[0].frame}: {bad[0].error()})", 5)
+
+    # per-kernel roofline leg: one instrumented eager frame in the same stream layout as the
+    # captured graph (side encoders and decoder chains concurrent, so a launch sees the CUs the
+    # side kernels hold, as in the replayed frame and in a rocprofv3 kernel trace of it), HIP
+    # events on the launching stream around every launch; grouped by (kernel kind, shape)
     groups = {}
     if rank == 0:
         ops.normalize_u8(frames[0], eng.x0)
-        eng.serial_side = True
-        eng.forward()                       # warm (no graph)
+        for _ in range(2):
+            eng.forward()                   # warm (no graph)
         ops.profile_begin()
         eng.forward()
         rec = ops.profile_end()
-        eng.serial_side = False
         for kind, flops, shape, kdt, ms in rec:
             k = groups.setdefault((kind, shape, kdt), {"launches": 0, "ms": 0.0, "flop": 0.0})
             k["launches"] += 1
@@ -265,7 +332,12 @@ def main():
         eng.finish_status()
         torch.cuda.synchronize()
         parity = depth_parity(depth, c, fov)
-        eng.check_status(block=True)     # every benched frame healthy (no timed-out hand-off, all finite)
+        if not args.ab:
+            eng.check_status(block=True)
+        if parity is None:
+            refuse("tests/golden/golden_forward_frame0.npz missing: depth L1 vs reference not measurable", 4)
+        if not args.ab and not parity["depth_rel_l1"] < parity["target"]:
+            refuse(f"depth rel-L1 {parity['depth_rel_l1']} >= {parity['target']} vs the reference", 4)
 
     if rank == 0:
         achieved = fps_per_gpu * FLOP_PER_FRAME / 1e12
@@ -297,6 +369,11 @@ def main():
             traffic = pmc_traffic(tile_kernel(tile, kdt), wgs) if tile_kernel(tile, kdt) else None
             if traffic is not None:
                 dom_info["traffic_source"] = traffic.pop("source")
+            rp = rocprof_avg_us(tile_kernel(tile, kdt)) if tile_kernel(tile, kdt) else None
+            if rp is not None:
+                # same kernel in the committed rocprofv3 summary (every launch of it in that bench run)
+                dom_info["rocprof"] = {"source": PROF_STATS, "avg_us": round(rp[0], 2), "calls": rp[1],
+                                       "frac": round(dom_flop / (rp[0] * 1e-6) / 1e12 / PEAK_BF16_TFLOPS, 4)}
         out = {
             "metric": "frames/sec at 1536x1536 (1/2/4/8 MI355X) + depth L1 vs reference",
             "value": round(fps, 3),
@@ -332,7 +409,11 @@ def main():
             "parity": parity,
             "setup_s": round(t_setup, 1),
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if args.ab:        # A/B timing run: not a bench result
+            out["metric"] = "A/B timing run (DP_GEMM_DEBUG / DP_ABLATE allowed): not a bench result"
+            out["ab_fps"], out["value"] = out["value"], None
+            out["ab_env"] = {v: os.environ.get(v, "") for v in ("DP_ABLATE", "DP_GEMM_DEBUG", "DP_ATTN_DEBUG")}
+        elif world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)
     if world > 1:

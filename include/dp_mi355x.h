@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 8
+#define DP_ABI_VERSION 9
 int dp_abi_version(void);
 
 /*
@@ -235,6 +235,15 @@ int dp_resize_bilinear(const void* src, int32_t src_dtype, int32_t C, int32_t H,
                        float* dst, int32_t OH, int32_t OW, dp_stream_t stream);
 
 /*
+ * dp_resize: dp_resize_bilinear with the F.interpolate mode DepthPro.infer passes through
+ * (`interpolation_mode`, depth_pro.py:243-279): DP_INTERP_BILINEAR, or DP_INTERP_BICUBIC
+ * (upsample_bicubic2d, align_corners=False, A = -0.75, border taps clamped).
+ */
+enum { DP_INTERP_BILINEAR = 0, DP_INTERP_BICUBIC = 1 };
+int dp_resize(const void* src, int32_t src_dtype, int32_t C, int32_t H, int32_t W, float* dst,
+              int32_t OH, int32_t OW, int32_t mode, dp_stream_t stream);
+
+/*
  * dp_patchify_pyramid: 1536^2 planar fp32 image -> im2col rows of the 35 sliding
  * windows [35*576][768] (k = c*256 + ky*16 + kx), building the 768^2 and 384^2
  * pyramid levels on the fly (the bilinear 0.5 / 0.25 resizes are exact 2x2 box
@@ -290,6 +299,12 @@ int dp_infer_epilogue(const float* canonical, int32_t src_h, int32_t src_w, cons
                       int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
                       float* f_px_out, int32_t* nonfinite, dp_stream_t stream);
 
+/* dp_infer_epilogue_mode: the same with the resize back to (H, W) in `mode` (DP_INTERP_*,
+ * depth_pro.py:288-291 passes interpolation_mode). */
+int dp_infer_epilogue_mode(const float* canonical, int32_t src_h, int32_t src_w, const float* fov_deg,
+                           int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
+                           float* f_px_out, int32_t* nonfinite, int32_t mode, dp_stream_t stream);
+
 /*
  * dp_resize_u8_cv: cv2.resize of an 8-bit HWC 3-channel frame to OH x OW -- the reference's
  * --downscale_factor (generate_depth_maps.py:95-110: INTER_AREA for factor < 1, INTER_LINEAR
@@ -315,6 +330,19 @@ int dp_resize_u8_cv(const uint8_t* src, int32_t H, int32_t W, uint8_t* dst, int3
 int dp_depth_to_points(const float* depth, int32_t H, int32_t W, const float* f_px_dev, double f_px,
                        int32_t use_given, const uint8_t* rgb_hwc, int32_t* row_offsets, double* xyz,
                        uint8_t* rgb_out, dp_stream_t stream);
+
+/*
+ * dp_depth_to_image: the frame loop's depth writers on the GPU (generate_depth_maps.py:15-44
+ * colorize_depth, :135-143 --raw): nanmin / nanmax of depth[n] into minmax (2 x uint32 scratch,
+ * order-preserving keys), then per pixel v = (d - min) / (max - min) in fp32 and
+ *   DP_DEPTH_IMG_COLOR: out uint8 [n][3] = lut[trunc(clip(v, 0, 1) * N)] (N -> N - 1; NaN -> entry
+ *     N + 2, matplotlib's "bad"); lut uint8 [(N + 3)][3] = (colormap lut * 255).astype(uint8);
+ *   DP_DEPTH_IMG_RAW16: out uint16 [n] = (uint16)(v * 65535) (NaN -> 0).
+ * Byte-identical to the reference's numpy / matplotlib arithmetic.
+ */
+enum { DP_DEPTH_IMG_COLOR = 0, DP_DEPTH_IMG_RAW16 = 1 };
+int dp_depth_to_image(const float* depth, int64_t n, uint32_t* minmax, const uint8_t* lut, int32_t lut_n,
+                      int32_t mode, void* out, dp_stream_t stream);
 
 #ifdef __cplusplus
 }

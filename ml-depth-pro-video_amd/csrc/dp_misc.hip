@@ -152,7 +152,58 @@ __device__ __forceinline__ float ld_any(const void* p, long long i) {
   else return KF16::to_f(((const u16*)p)[i]);
 }
 
-template <int SRC>
+// PyTorch upsample_bicubic2d, align_corners=False (A = -0.75): src = scale*(dst+0.5)-0.5 NOT
+// clamped, i0 = floor(src), t = src - i0, taps i0-1 .. i0+2 clamped to [0, in-1] (bounded access).
+__device__ __forceinline__ void cubic_coeffs(float t, float (&c)[4]) {
+  constexpr float A = -0.75f;
+  auto cc1 = [](float x) { return ((A + 2.f) * x - (A + 3.f)) * x * x + 1.f; };          // |x| <= 1
+  auto cc2 = [](float x) { return ((A * x - 5.f * A) * x + 8.f * A) * x - 4.f * A; };    // 1 < |x| < 2
+  c[0] = cc2(t + 1.f);
+  c[1] = cc1(t);
+  c[2] = cc1(1.f - t);
+  c[3] = cc2(2.f - t);
+}
+__device__ __forceinline__ void cubic_index(int d, float scale, int in, int (&i)[4], float (&c)[4]) {
+  const float s = scale * ((float)d + 0.5f) - 0.5f;
+  const float f = floorf(s);
+  const int i0 = (int)f;
+  cubic_coeffs(s - f, c);
+  #pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int v = i0 - 1 + k;
+    i[k] = v < 0 ? 0 : (v > in - 1 ? in - 1 : v);
+  }
+}
+
+// One output pixel of plane `p` (H x W, element loader ld(i)) at (oy, ox): MODE 0 bilinear, 1 bicubic,
+// each value pre-multiplied by `mul` (the infer epilogue's scale, applied before the resize as there).
+template <int MODE, typename LD>
+__device__ __forceinline__ float resample(LD ld, int H, int W, int oy, int ox, float sh, float sw, float mul) {
+  if constexpr (MODE == DP_INTERP_BILINEAR) {
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    src_index(oy, sh, H, y0, y1, ly0, ly1);
+    src_index(ox, sw, W, x0, x1, lx0, lx1);
+    const float v00 = ld((long long)y0 * W + x0) * mul, v01 = ld((long long)y0 * W + x1) * mul;
+    const float v10 = ld((long long)y1 * W + x0) * mul, v11 = ld((long long)y1 * W + x1) * mul;
+    return ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+  } else {
+    int yi[4], xi[4];
+    float cy[4], cx[4];
+    cubic_index(oy, sh, H, yi, cy);
+    cubic_index(ox, sw, W, xi, cx);
+    float r[4];
+    #pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long long row = (long long)yi[k] * W;
+      r[k] = ld(row + xi[0]) * mul * cx[0] + ld(row + xi[1]) * mul * cx[1] + ld(row + xi[2]) * mul * cx[2] +
+             ld(row + xi[3]) * mul * cx[3];
+    }
+    return r[0] * cy[0] + r[1] * cy[1] + r[2] * cy[2] + r[3] * cy[3];
+  }
+}
+
+template <int SRC, int MODE>
 __global__ void resize_kernel(const void* __restrict__ src, int C, int H, int W, float* __restrict__ dst,
                               int OH, int OW, float sh, float sw) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -161,16 +212,8 @@ __global__ void resize_kernel(const void* __restrict__ src, int C, int H, int W,
   const int ox = i % OW;
   const int oy = (i / OW) % OH;
   const int c = i / ((long long)OW * OH);
-  int y0, y1, x0, x1;
-  float ly0, ly1, lx0, lx1;
-  src_index(oy, sh, H, y0, y1, ly0, ly1);
-  src_index(ox, sw, W, x0, x1, lx0, lx1);
   const long long pb = (long long)c * H * W;
-  const float v00 = ld_any<SRC>(src, pb + (long long)y0 * W + x0);
-  const float v01 = ld_any<SRC>(src, pb + (long long)y0 * W + x1);
-  const float v10 = ld_any<SRC>(src, pb + (long long)y1 * W + x0);
-  const float v11 = ld_any<SRC>(src, pb + (long long)y1 * W + x1);
-  dst[i] = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+  dst[i] = resample<MODE>([&](long long j) { return ld_any<SRC>(src, pb + j); }, H, W, oy, ox, sh, sw, 1.f);
 }
 
 // ------------------------------------------- pyramid + sliding windows + im2col
@@ -301,6 +344,7 @@ __global__ void fov_tail_kernel(const u16* __restrict__ x6, const float* __restr
 }
 
 // ------------------------------------------------------------ infer epilogue
+template <int MODE>
 __global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW, const float* __restrict__ fov,
                                  int use_given, float given_scale, float given_fpx, int H, int W,
                                  float* __restrict__ depth, float* __restrict__ fpx_out, int* __restrict__ nonfinite) {
@@ -325,13 +369,8 @@ __global__ void infer_epi_kernel(const float* __restrict__ canon, int SH, int SW
     v = canon[i] * scale;
   } else {
     const int ox = i % W, oy = i / W;
-    int y0, y1, x0, x1;
-    float ly0, ly1, lx0, lx1;
-    src_index(oy, (float)SH / (float)H, SH, y0, y1, ly0, ly1);
-    src_index(ox, (float)SW / (float)W, SW, x0, x1, lx0, lx1);
-    const float v00 = canon[(long long)y0 * SW + x0] * scale, v01 = canon[(long long)y0 * SW + x1] * scale;
-    const float v10 = canon[(long long)y1 * SW + x0] * scale, v11 = canon[(long long)y1 * SW + x1] * scale;
-    v = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+    v = resample<MODE>([&](long long j) { return canon[j]; }, SH, SW, oy, ox, (float)SH / (float)H,
+                       (float)SW / (float)W, scale);
   }
   // torch.clamp keeps a NaN a NaN (fminf / fmaxf alone would turn it into a bound)
   v = v != v ? v : fminf(fmaxf(v, 1e-4f), 1e4f);
@@ -500,20 +539,30 @@ extern "C" int dp_normalize_u8(const uint8_t* img, int32_t H, int32_t W, void* o
   return 0;
 }
 
-extern "C" int dp_resize_bilinear(const void* src, int32_t src_dtype, int32_t C, int32_t H, int32_t W, float* dst,
-                                  int32_t OH, int32_t OW, dp_stream_t stream) {
+extern "C" int dp_resize(const void* src, int32_t src_dtype, int32_t C, int32_t H, int32_t W, float* dst,
+                         int32_t OH, int32_t OW, int32_t mode, dp_stream_t stream) {
   if (!src || !dst) return DP_ERR_ARG;
   if (C <= 0 || H <= 0 || W <= 0 || OH <= 0 || OW <= 0) return DP_ERR_SHAPE;
+  if (mode != DP_INTERP_BILINEAR && mode != DP_INTERP_BICUBIC) return DP_ERR_ARG;
   const long long total = (long long)C * OH * OW;
   const float sh = (float)H / (float)OH, sw = (float)W / (float)OW;
   hipStream_t s = (hipStream_t)stream;
   dim3 g(blocks_for(total, 256));
-  if (src_dtype == DP_F32) hipLaunchKernelGGL(resize_kernel<DP_F32>, g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw);
-  else if (src_dtype == DP_BF16) hipLaunchKernelGGL(resize_kernel<DP_BF16>, g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw);
-  else if (src_dtype == DP_F16) hipLaunchKernelGGL(resize_kernel<DP_F16>, g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw);
-  else return DP_ERR_DTYPE;
+#define DP_RS(M_) do { \
+    if (src_dtype == DP_F32) hipLaunchKernelGGL((resize_kernel<DP_F32, M_>), g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw); \
+    else if (src_dtype == DP_BF16) hipLaunchKernelGGL((resize_kernel<DP_BF16, M_>), g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw); \
+    else if (src_dtype == DP_F16) hipLaunchKernelGGL((resize_kernel<DP_F16, M_>), g, dim3(256), 0, s, src, C, H, W, dst, OH, OW, sh, sw); \
+    else return DP_ERR_DTYPE; } while (0)
+  if (mode == DP_INTERP_BILINEAR) DP_RS(DP_INTERP_BILINEAR);
+  else DP_RS(DP_INTERP_BICUBIC);
+#undef DP_RS
   DP_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int dp_resize_bilinear(const void* src, int32_t src_dtype, int32_t C, int32_t H, int32_t W, float* dst,
+                                  int32_t OH, int32_t OW, dp_stream_t stream) {
+  return dp_resize(src, src_dtype, C, H, W, dst, OH, OW, DP_INTERP_BILINEAR, stream);
 }
 
 extern "C" int dp_patchify_pyramid(const float* x0, void* cols, int32_t dtype, dp_stream_t stream) {
@@ -575,18 +624,30 @@ extern "C" int dp_fov_tail(const void* x6, int32_t dtype, const float* w, float 
   return 0;
 }
 
+extern "C" int dp_infer_epilogue_mode(const float* canonical, int32_t SH, int32_t SW, const float* fov_deg,
+                                      int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
+                                      float* f_px_out, int32_t* nonfinite, int32_t mode, dp_stream_t stream) {
+  if (!canonical || !depth || (!use_given && !fov_deg)) return DP_ERR_ARG;
+  if (H <= 0 || W <= 0 || SH <= 0 || SW <= 0) return DP_ERR_SHAPE;
+  if (mode != DP_INTERP_BILINEAR && mode != DP_INTERP_BICUBIC) return DP_ERR_ARG;
+  // reference: inverse_depth = canonical * (W / f_px) with W / f_px a Python (double) scalar
+  const float given_scale = use_given ? (float)((double)W / f_given) : 0.f;
+  dim3 g(blocks_for((long long)H * W, 256));
+  if (mode == DP_INTERP_BILINEAR)
+    hipLaunchKernelGGL(infer_epi_kernel<DP_INTERP_BILINEAR>, g, dim3(256), 0, (hipStream_t)stream, canonical, SH, SW,
+                       fov_deg, use_given, given_scale, (float)f_given, H, W, depth, f_px_out, (int*)nonfinite);
+  else
+    hipLaunchKernelGGL(infer_epi_kernel<DP_INTERP_BICUBIC>, g, dim3(256), 0, (hipStream_t)stream, canonical, SH, SW,
+                       fov_deg, use_given, given_scale, (float)f_given, H, W, depth, f_px_out, (int*)nonfinite);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int dp_infer_epilogue(const float* canonical, int32_t SH, int32_t SW, const float* fov_deg,
                                  int32_t use_given, double f_given, int32_t H, int32_t W, float* depth,
                                  float* f_px_out, int32_t* nonfinite, dp_stream_t stream) {
-  if (!canonical || !depth || (!use_given && !fov_deg)) return DP_ERR_ARG;
-  if (H <= 0 || W <= 0 || SH <= 0 || SW <= 0) return DP_ERR_SHAPE;
-  // reference: inverse_depth = canonical * (W / f_px) with W / f_px a Python (double) scalar
-  const float given_scale = use_given ? (float)((double)W / f_given) : 0.f;
-  hipLaunchKernelGGL(infer_epi_kernel, dim3(blocks_for((long long)H * W, 256)), dim3(256), 0, (hipStream_t)stream,
-                     canonical, SH, SW, fov_deg, use_given, given_scale, (float)f_given, H, W, depth, f_px_out,
-                     (int*)nonfinite);
-  DP_CHECK_LAUNCH();
-  return 0;
+  return dp_infer_epilogue_mode(canonical, SH, SW, fov_deg, use_given, f_given, H, W, depth, f_px_out, nonfinite,
+                                DP_INTERP_BILINEAR, stream);
 }
 
 extern "C" int dp_resize_u8_cv(const uint8_t* src, int32_t H, int32_t W, uint8_t* dst, int32_t OH, int32_t OW,
@@ -711,7 +772,117 @@ __global__ void __launch_bounds__(256) pts_scatter_kernel(const float* __restric
   }
 }
 
+
+// ------------------------------------------------- depth map -> 8-bit colour / 16-bit grey
+// The frame loop's writers (reference generate_depth_maps.py:15-44 colorize_depth, :135-143 --raw)
+// on the GPU: nanmin / nanmax of the depth map (order-preserving integer keys, NaN skipped), then
+// per pixel n = (d - min) / (max - min) in fp32 (IEEE division, as numpy's float32 arithmetic),
+// colour: np.clip(n, 0, 1), matplotlib Colormap.__call__'s index trunc(n * N) (N -> N - 1, NaN ->
+// the "bad" entry) into the colormap's byte table (host-built: (lut * 255).astype(uint8));
+// raw: (uint16)(n * 65535) (NaN -> 0, numpy's cast on x86).
+__device__ __forceinline__ uint32_t order_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_float(uint32_t k) {   // inverse of order_key; 0xffffffff / 0 -> NaN
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__global__ void minmax_init_kernel(uint32_t* __restrict__ mm) {
+  if (threadIdx.x < 2) mm[threadIdx.x] = threadIdx.x == 0 ? 0xffffffffu : 0u;
+}
+
+__global__ void __launch_bounds__(256) minmax_kernel(const float* __restrict__ d, long long n, uint32_t* __restrict__ mm) {
+  __shared__ uint32_t red[2][4];
+  uint32_t kmin = 0xffffffffu, kmax = 0u;
+  const long long stride = (long long)gridDim.x * 256 * 4;
+  for (long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += stride) {
+    float v[4];
+    if (i + 3 < n && ((uintptr_t)(d + i) & 15) == 0) {
+      const float4 q = *(const float4*)(d + i);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = i + r < n ? d[i + r] : __builtin_nanf("");
+    }
+    #pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (v[r] == v[r]) {
+        const uint32_t k = order_key(v[r]);
+        kmin = k < kmin ? k : kmin;
+        kmax = k > kmax ? k : kmax;
+      }
+    }
+  }
+  #pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t a = __shfl_xor(kmin, o), b = __shfl_xor(kmax, o);
+    kmin = a < kmin ? a : kmin;
+    kmax = b > kmax ? b : kmax;
+  }
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = kmin; red[1][threadIdx.x >> 6] = kmax; }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    uint32_t a = red[0][threadIdx.x & 3], b = red[1][threadIdx.x & 3];
+    #pragma unroll
+    for (int o = 2; o > 0; o >>= 1) {
+      const uint32_t a2 = __shfl_xor(a, o), b2 = __shfl_xor(b, o);
+      a = a2 < a ? a2 : a;
+      b = b2 > b ? b2 : b;
+    }
+    if (threadIdx.x == 0) {
+      atomicMin(mm, a);
+      atomicMax(mm + 1, b);
+    }
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) depth_color_kernel(const float* __restrict__ d, long long n,
+                                                          const uint32_t* __restrict__ mm, const uint8_t* __restrict__ lut,
+                                                          int N, void* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float mn = key_float(mm[0]), mx = key_float(mm[1]);
+  const float v = (d[i] - mn) / (mx - mn);
+  if constexpr (MODE == 0) {
+    int idx;
+    if (v != v) {
+      idx = N + 2;                                   // matplotlib's _i_bad
+    } else {
+      float x = fminf(fmaxf(v, 0.f), 1.f) * (float)N;
+      if (x == (float)N) x = (float)(N - 1);
+      idx = (int)x;
+    }
+    uint8_t* o = (uint8_t*)out + 3 * i;
+    o[0] = lut[3 * idx];
+    o[1] = lut[3 * idx + 1];
+    o[2] = lut[3 * idx + 2];
+  } else {
+    const float r = v * 65535.f;
+    ((uint16_t*)out)[i] = r == r ? (uint16_t)(int)r : (uint16_t)0;
+  }
+}
 }  // namespace
+
+extern "C" int dp_depth_to_image(const float* depth, int64_t n, uint32_t* minmax, const uint8_t* lut, int32_t lut_n,
+                                 int32_t mode, void* out, dp_stream_t stream) {
+  if (!depth || !minmax || !out || (mode == DP_DEPTH_IMG_COLOR && (!lut || lut_n <= 0))) return DP_ERR_ARG;
+  if (mode != DP_DEPTH_IMG_COLOR && mode != DP_DEPTH_IMG_RAW16) return DP_ERR_ARG;
+  if (n <= 0) return DP_ERR_SHAPE;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(minmax_init_kernel, dim3(1), dim3(64), 0, s, minmax);
+  const int g = (int)(n / 1024 + 1 < 1024 ? n / 1024 + 1 : 1024);
+  hipLaunchKernelGGL(minmax_kernel, dim3(g), dim3(256), 0, s, depth, (long long)n, minmax);
+  if (mode == DP_DEPTH_IMG_COLOR)
+    hipLaunchKernelGGL(depth_color_kernel<0>, dim3(blocks_for(n, 256)), dim3(256), 0, s, depth, (long long)n, minmax,
+                       lut, lut_n, out);
+  else
+    hipLaunchKernelGGL(depth_color_kernel<1>, dim3(blocks_for(n, 256)), dim3(256), 0, s, depth, (long long)n, minmax,
+                       lut, lut_n, out);
+  DP_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dp_depth_to_points(const float* depth, int32_t H, int32_t W, const float* f_px_dev, double f_px,
                                   int32_t use_given, const uint8_t* rgb_hwc, int32_t* row_offsets, double* xyz,

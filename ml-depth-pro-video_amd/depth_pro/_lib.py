@@ -18,12 +18,15 @@ DP_ACT_NONE, DP_ACT_RELU, DP_ACT_GELU = 0, 1, 2
 DP_A_DENSE, DP_A_CONV = 0, 1
 DP_STORE_ROWS, DP_STORE_DECONV2X2, DP_STORE_HEAD_PS = 0, 1, 2
 DP_CV_INTER_LINEAR, DP_CV_INTER_AREA = 1, 3
+DP_INTERP_BILINEAR, DP_INTERP_BICUBIC = 0, 1
+DP_DEPTH_IMG_COLOR, DP_DEPTH_IMG_RAW16 = 0, 1
+INTERP_MODES = {"bilinear": DP_INTERP_BILINEAR, "bicubic": DP_INTERP_BICUBIC}
 (DP_TILE_AUTO, DP_TILE_128x128, DP_TILE_256x64, DP_TILE_256x32, DP_TILE_BIG_256x256, DP_TILE_BIG_256x128,
  DP_TILE_BIG_256x256_K32, DP_TILE_BIG_256x128_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
  DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128,
  DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256) = range(21)
-DP_ABI_VERSION = 8
+DP_ABI_VERSION = 9
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -35,9 +38,9 @@ LIB_PATH = os.environ.get(
 EXPORTS = (
     "dp_abi_version", "dp_gemm", "dp_gemm_grouped", "dp_layernorm", "dp_layernorm_grouped", "dp_attention",
     "dp_attention_log2q", "dp_normalize_u8",
-    "dp_resize_bilinear", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
-    "dp_merge_windows_range", "dp_fov_tail", "dp_infer_epilogue", "dp_gemm_workspace_size", "dp_gemm_plan",
-    "dp_depth_to_points", "dp_gemm_workspace_check", "dp_resize_u8_cv",
+    "dp_resize_bilinear", "dp_resize", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
+    "dp_merge_windows_range", "dp_fov_tail", "dp_infer_epilogue", "dp_infer_epilogue_mode", "dp_gemm_workspace_size", "dp_gemm_plan",
+    "dp_depth_to_points", "dp_gemm_workspace_check", "dp_resize_u8_cv", "dp_depth_to_image",
 )
 
 
@@ -103,16 +106,19 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "dp_attention_log2q": [vp, vp, i32, i32, i32, i32, i32, vp],
         "dp_normalize_u8": [vp, i32, i32, vp, i32, vp],
         "dp_resize_bilinear": [vp, i32, i32, i32, i32, vp, i32, i32, vp],
+        "dp_resize": [vp, i32, i32, i32, i32, vp, i32, i32, i32, vp],
         "dp_patchify_pyramid": [vp, vp, i32, vp],
         "dp_vit_cls_rows": [vp, vp, vp, i32, vp],
         "dp_merge_windows": [vp, i32, i64, i32, i32, i32, vp, i32, vp],
         "dp_merge_windows_range": [vp, i32, i64, i32, i32, i32, i32, i32, vp, i32, vp],
         "dp_fov_tail": [vp, i32, vp, f32, vp, vp],
         "dp_infer_epilogue": [vp, i32, i32, vp, i32, f64, i32, i32, vp, vp, vp, vp],
+        "dp_infer_epilogue_mode": [vp, i32, i32, vp, i32, f64, i32, i32, vp, vp, vp, i32, vp],
         "dp_gemm_workspace_size": [],
         "dp_gemm_workspace_check": [vp, vp, vp],
         "dp_resize_u8_cv": [vp, i32, i32, vp, i32, i32, i32, vp],
         "dp_depth_to_points": [vp, i32, i32, vp, f64, i32, vp, vp, vp, vp, vp],
+        "dp_depth_to_image": [vp, i64, vp, vp, i32, i32, vp, vp],
         "dp_gemm_plan": [ctypes.POINTER(GemmArgs), ctypes.POINTER(i32), ctypes.POINTER(i32)],
     }
     for name, argtypes in sig.items():

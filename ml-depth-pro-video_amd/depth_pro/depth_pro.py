@@ -13,7 +13,13 @@ AssertionError for a non-1536^2 `forward` input).  Differences, by design:
     DEPTH_PRO_COMPUTE_DTYPE=bf16|fp16|mixed to override); a CPU device or a
     missing library raises instead of computing anything on the host;
   * with `checkpoint_uri=None` the weights are the deterministic synthetic set
-    of `depth_pro.weights` (the reference leaves PyTorch's random init).
+    of `depth_pro.weights` (the reference leaves PyTorch's random init);
+  * the fp32 parameters stay in host memory: `model.to(device)` / `.cuda()` only pick
+    the device the engine runs on, and the engine packs its 16-bit GEMM-ready weight
+    set straight from the host tensors (no fp32 copy of the 952 M parameters in HBM);
+  * a bad frame (timed-out stream-K hand-off, NaN / inf output) is reported without
+    stalling the stream: `last_status().check()` for the last call, and every later
+    `infer` / `forward` call raises DPError for an earlier bad frame nobody checked.
 """
 
 from __future__ import annotations
@@ -28,7 +34,7 @@ from torch import nn
 
 from . import ops
 from ._lib import DP_BF16, DP_F16, DPError, load
-from .engine import Engine, pack_weights
+from .engine import BatchStatus, Engine, pack_weights
 from .spec import IMG_SIZE, param_spec
 from .weights import synthetic_state_dict
 
@@ -150,16 +156,35 @@ class DepthPro(nn.Module):
         self.use_fov_head = use_fov_head
         self.compute_dtype = compute_dtype
         self._engine: Optional[Engine] = None
+        self._device: torch.device = torch.device(device)      # where the engine runs
         self._packed_device: Optional[torch.device] = None   # set by from_packed (meta parameters)
         self._use_graph = os.environ.get("DEPTH_PRO_HIPGRAPH", "0") == "1"
+        self._last_status = None
 
     # -- engine lifecycle
     def _invalidate(self):
         self._engine = None
 
     def _apply(self, fn, *a, **k):
-        self._invalidate()
-        return super()._apply(fn, *a, **k)
+        """`.to(device)` / `.cuda()` / `.half()` (nn.Module._apply): the parameters stay in host
+        memory as loaded (fp32); a new device re-targets the engine (packed on next use) and a
+        dtype change is a no-op -- the compute precision is `compute_dtype`, fixed at creation
+        (create_model_and_transforms' `precision`, as the reference's model.half())."""
+        if self._packed_device is not None:
+            return self
+        try:
+            fn(torch.empty(0, device="meta"))      # dtype-only (.half(), .float()): stays on meta
+            return self
+        except (NotImplementedError, RuntimeError):
+            pass                                    # a device move: copying out of meta fails
+        self._retarget(fn(torch.empty(0)).device)
+        return self
+
+    def _retarget(self, dev) -> None:
+        dev = torch.device(dev)
+        if dev != self._device:
+            self._device = dev
+            self._invalidate()
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         self._invalidate()
@@ -175,7 +200,7 @@ class DepthPro(nn.Module):
         device = torch.device(device)
         if device.type == "cuda" and device.index is None:   # 'cuda' -> the current device, as tensors get
             device = torch.device("cuda", torch.cuda.current_device())
-        m._packed_device = device
+        m._packed_device = m._device = device
         m._engine = Engine(packed, m._packed_device, compute_dtype, use_fov=use_fov_head)
         m.eval()
         return m
@@ -185,12 +210,16 @@ class DepthPro(nn.Module):
             if self._packed_device is not None:
                 raise DPError("this DepthPro was built from packed weights (from_packed); its parameters are "
                               "placeholders, so the engine cannot be rebuilt from them")
-            dev = next(self.parameters()).device
+            dev = self._device
+            if dev.type == "cuda" and dev.index is None:      # 'cuda' -> the current device
+                dev = self._device = torch.device("cuda", torch.cuda.current_device())
             if dev.type != "cuda":
                 raise DPError("DepthPro (MI355X engine) runs on a ROCm device; got device "
                               f"{dev} -- there is no CPU path")
             load()
             with torch.no_grad():
+                # straight from the host tensors: each is uploaded, converted to its packed 16-bit
+                # layout and dropped, so only the packed set stays in HBM
                 packed = pack_weights(dict(self.state_dict()), dev, self.compute_dtype)
             self._engine = Engine(packed, dev, self.compute_dtype, use_fov=self.use_fov_head)
             if self._use_graph:
@@ -212,30 +241,41 @@ class DepthPro(nn.Module):
         """Return the internal image size of the network (1536)."""
         return IMG_SIZE
 
-    def _run_frame(self, x3: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        """x3: (3, S, S) network-resolution frame on device -> engine outputs (static buffers)."""
+    def _run_frame(self, x3: torch.Tensor):
+        """x3: (3, S, S) network-resolution frame on device -> (engine outputs (static buffers),
+        FrameStatus)."""
         eng = self.engine()
-        ops.resize_bilinear(x3, eng.x0)  # dtype conversion / copy into the static input
+        ops.resize(x3, eng.x0)  # dtype conversion / copy into the static input
         out = eng.run()
-        eng.finish_status()
-        return out
+        return out, eng.finish_status()
 
     def last_status(self):
-        """FrameStatus of the most recent frame this model ran (`engine.FrameStatus`): `.check()`
-        raises DPError if that frame's outputs are invalid (a timed-out stream-K hand-off, or NaN /
-        inf in depth or focal length) -- waiting for that frame only.  The frame loops call it
-        before writing a frame's files."""
-        return self.engine().last_status
+        """Status of the most recent `infer` / `forward` call (`engine.BatchStatus` over its frames):
+        `.check()` raises DPError naming every invalid frame of that call (a timed-out stream-K
+        hand-off, or NaN / inf in depth or focal length) -- waiting for those frames only.  The
+        frame loops call it before writing a frame's files."""
+        if self._last_status is None:
+            return self.engine().last_status
+        return self._last_status
+
+    def _check_earlier(self, eng: Engine) -> None:
+        """Non-blocking health check of earlier frames: a finished bad frame that no
+        caller has checked raises here, on the next call, instead of going unnoticed."""
+        eng.check_status(block=False)
 
     def forward(self, x: torch.Tensor) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         """Canonical inverse depth (B,1,1536,1536) and FOV in degrees (B,1,1,1)."""
         _, _, H, W = x.shape
         assert H == self.img_size and W == self.img_size
-        outs, fovs = [], []
+        eng = self.engine()
+        self._check_earlier(eng)
+        outs, fovs, sts = [], [], []
         for b in range(x.shape[0]):
-            canonical, fov = self._run_frame(x[b])
+            (canonical, fov), st = self._run_frame(x[b])
             outs.append(canonical.clone())
             fovs.append(fov.clone())
+            sts.append(st)
+        self._last_status = BatchStatus(sts)
         canonical = torch.cat(outs, 0)
         fov_deg = torch.cat(fovs, 0) if self.use_fov_head else None
         return canonical, fov_deg
@@ -251,10 +291,10 @@ class DepthPro(nn.Module):
 
         x: (3,H,W) or (B,3,H,W).  As in the reference, a batch gives depth (B,H,W) and,
         without a given f_px, one focal length per frame (B,); frames run one at a time
-        through the engine (each a full 1536^2 forward).
+        through the engine (each a full 1536^2 forward).  `interpolation_mode` is the
+        F.interpolate mode of both resizes (to 1536^2 and back): "bilinear" or "bicubic".
         """
-        if interpolation_mode != "bilinear":
-            raise NotImplementedError("only interpolation_mode='bilinear' (the reference default) is supported")
+        mode_ok = ops.interp_mode(interpolation_mode)  # noqa: F841  (ValueError for another mode)
         if len(x.shape) == 3:
             x = x.unsqueeze(0)
         B, _, H, W = x.shape
@@ -263,21 +303,24 @@ class DepthPro(nn.Module):
             raise DPError(f"input on {x.device}, model on {eng.dev}")
         if f_px is None and not self.use_fov_head:
             raise TypeError("f_px is required when the model has no FOV head")
+        self._check_earlier(eng)
         given = None
         if f_px is not None:
             given = float(f_px.detach().float().reshape(-1)[0].item()) if torch.is_tensor(f_px) else float(f_px)
         depth = torch.empty(B, H, W, dtype=torch.float32, device=x.device)
         f_out = torch.empty(B, dtype=torch.float32, device=x.device) if f_px is None else None
+        sts = []
         for b in range(B):
             # prologue: (resize to) 1536^2 fp32 straight into the engine's static input
-            ops.resize_bilinear(x[b], eng.x0)
+            ops.resize(x[b], eng.x0, interpolation_mode)
             canonical, fov_deg = eng.run()
             bad = eng.status_dev[-1:]     # NaN / inf outputs of this frame (FrameStatus)
             if f_px is None:
-                ops.infer_epilogue(canonical, fov_deg, None, H, W, depth[b], f_out[b], bad)
+                ops.infer_epilogue(canonical, fov_deg, None, H, W, depth[b], f_out[b], bad, mode=interpolation_mode)
             else:
-                ops.infer_epilogue(canonical, None, given, H, W, depth[b], None, bad)
-            eng.finish_status()
+                ops.infer_epilogue(canonical, None, given, H, W, depth[b], None, bad, mode=interpolation_mode)
+            sts.append(eng.finish_status())
+        self._last_status = BatchStatus(sts)
         if f_px is None:
             f_px = f_out.squeeze()
         else:
@@ -317,9 +360,9 @@ def create_model_and_transforms(
     if len(missing_keys) != 0:
         raise KeyError(f"Keys are missing when loading monodepth: {missing_keys}")
     del state_dict
-    model = model.to(device)
-    if precision == torch.half:
-        model.half()
+    # the engine's device; the fp32 parameters stay on the host (DepthPro._apply), and
+    # precision == torch.half (the reference's model.half()) is already the f16 compute_dtype
+    model._retarget(device)
     model.eval()
     transform = Transform(device, precision)
     return model, transform

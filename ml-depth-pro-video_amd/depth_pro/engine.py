@@ -241,12 +241,14 @@ class FrameStatus:
     `Engine.finish_status` copies the words into pinned host memory on the same stream.
     `check()` waits for that frame's copy only and raises DPError if the frame is bad, so a caller
     that checks before writing a frame's files drops exactly the bad frame (generate_depth_maps,
-    depth-pro-run)."""
+    depth-pro-run).  A status is reported once: after `check()` (or `Engine.check_status`) has
+    seen it, later `check_status` sweeps skip it."""
 
     def __init__(self, frame: int, words: torch.Tensor, event: torch.cuda.Event):
         self.frame = frame
         self.words = words            # pinned int32: [workspace error words..., non-finite count]
         self.event = event
+        self.reported = False
 
     def ready(self) -> bool:
         return self.event.query()
@@ -264,8 +266,38 @@ class FrameStatus:
 
     def check(self) -> None:
         msg = self.error()
+        self.reported = True
         if msg is not None:
             raise DPError(f"frame {self.frame}: {msg}")
+
+
+class BatchStatus:
+    """The FrameStatus of every frame of one `DepthPro.infer` / `forward` call, as one status:
+    bad if any frame is; `check()` raises naming every bad frame (last_status() of a batched call)."""
+
+    def __init__(self, frames: list):
+        self.frames = list(frames)
+        self.frame = self.frames[-1].frame if self.frames else -1
+
+    @property
+    def reported(self) -> bool:
+        return all(f.reported for f in self.frames)
+
+    def ready(self) -> bool:
+        return all(f.ready() for f in self.frames)
+
+    def error(self) -> Optional[str]:
+        bad = [(f.frame, e) for f in self.frames for e in [f.error()] if e is not None]
+        if not bad:
+            return None
+        return "; ".join(f"frame {n}: {e}" for n, e in bad)
+
+    def check(self) -> None:
+        msg = self.error()
+        for f in self.frames:
+            f.reported = True
+        if msg is not None:
+            raise DPError(msg)
 
 
 class Engine:
@@ -368,7 +400,8 @@ class Engine:
         self._wss = [self.ws_main, self.ws_dec]
         self.status_dev = torch.zeros(len(self._wss) + 1, dtype=torch.int32, device=dev)
         self._frames = 0
-        self._recent: list = []           # FrameStatus of the last frames (check_status)
+        self._recent: list = []           # FrameStatus of the frames not checked yet (check_status)
+        self._unreported: list = []       # finished bad frames owed to the next check_status
         self.last_status: Optional[FrameStatus] = None
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
 
@@ -644,27 +677,38 @@ class Engine:
         ev.record()
         st = FrameStatus(self._frames, words, ev)
         self._frames += 1
-        self._recent = (self._recent + [st])[-64:]
+        self._recent.append(st)
+        if len(self._recent) > 64:
+            # bounded list: move finished frames out (bad ones stay owed to the next check_status);
+            # if none has finished, wait for the oldest
+            self._sweep(block_oldest=True)
         self.last_status = st
         if self.sync_check:
             st.check()
         return st
 
-    def check_status(self, block: bool = True) -> None:
-        """Raise DPError if one of the recent frames not checked yet is bad (block=False: only
-        frames already done).  Each frame's status is reported once: checked frames leave the
-        list, so a bad frame does not fail every later check."""
+    def _sweep(self, block: bool = False, block_oldest: bool = False) -> None:
         keep = []
-        bad = None
-        for st in self._recent:
-            if block or st.ready():
-                if bad is None and st.error() is not None:
-                    bad = st
+        for j, st in enumerate(self._recent):
+            if st.reported:
+                continue
+            if block or st.ready() or (block_oldest and j == 0):
+                if st.error() is not None:
+                    self._unreported.append(st)
             else:
                 keep.append(st)
         self._recent = keep
-        if bad is not None:
-            bad.check()
+
+    def check_status(self, block: bool = True) -> None:
+        """Raise DPError naming EVERY bad frame not reported yet (block=False: only frames already
+        done).  Each frame's status is reported once: checked frames leave the list, so a bad
+        frame does not fail every later check."""
+        self._sweep(block=block)
+        bad, self._unreported = [st for st in self._unreported if not st.reported], []
+        if bad:
+            for st in bad:
+                st.reported = True
+            raise DPError("; ".join(f"frame {st.frame}: {st.error()}" for st in bad))
 
 
 class _StreamCtx:

@@ -313,12 +313,25 @@ def normalize_u8(img: torch.Tensor, out: torch.Tensor) -> None:
                                       _stream(out)), "dp_normalize_u8")
 
 
-def resize_bilinear(src: torch.Tensor, dst: torch.Tensor) -> None:
+def interp_mode(mode: str) -> int:
+    """F.interpolate mode name -> DP_INTERP_* (the modes DepthPro.infer can pass with
+    align_corners=False: bilinear, bicubic)."""
+    if mode not in _lib.INTERP_MODES:
+        raise ValueError(f"interpolation_mode={mode!r}: expected one of {sorted(_lib.INTERP_MODES)}")
+    return _lib.INTERP_MODES[mode]
+
+
+def resize(src: torch.Tensor, dst: torch.Tensor, mode: str = "bilinear") -> None:
+    """dp_resize: planar (C,H,W) -> dst (C,OH,OW) fp32, F.interpolate(mode, align_corners=False)."""
     src = src.contiguous()
     C, H, W = src.shape[-3:]
     OH, OW = dst.shape[-2:]
-    check(_lib.load().dp_resize_bilinear(src.data_ptr(), dtype_code(src.dtype), C, H, W, dst.data_ptr(),
-                                         OH, OW, _stream(dst)), "dp_resize_bilinear")
+    check(_lib.load().dp_resize(src.data_ptr(), dtype_code(src.dtype), C, H, W, dst.data_ptr(),
+                                OH, OW, interp_mode(mode), _stream(dst)), "dp_resize")
+
+
+def resize_bilinear(src: torch.Tensor, dst: torch.Tensor) -> None:
+    resize(src, dst, "bilinear")
 
 
 def patchify_pyramid(x0: torch.Tensor, cols: torch.Tensor) -> None:
@@ -351,13 +364,15 @@ def fov_tail(x6: torch.Tensor, w: torch.Tensor, bias: float, out: torch.Tensor) 
 
 def infer_epilogue(canonical: torch.Tensor, fov_deg: Optional[torch.Tensor], f_given: Optional[float],
                    H: int, W: int, depth: torch.Tensor, f_px_out: Optional[torch.Tensor],
-                   nonfinite: Optional[torch.Tensor] = None) -> None:
-    """dp_infer_epilogue; `nonfinite` (device int32, optional) counts NaN / inf outputs."""
+                   nonfinite: Optional[torch.Tensor] = None, mode: str = "bilinear") -> None:
+    """dp_infer_epilogue_mode; `nonfinite` (device int32, optional) counts NaN / inf outputs;
+    `mode` the F.interpolate mode of the resize back to (H, W)."""
     SH, SW = canonical.shape[-2:]
     use_given = f_given is not None
-    check(_lib.load().dp_infer_epilogue(canonical.data_ptr(), SH, SW, _p(fov_deg), int(use_given),
-                                        float(f_given) if use_given else 0.0, H, W, depth.data_ptr(),
-                                        _p(f_px_out), _p(nonfinite), _stream(depth)), "dp_infer_epilogue")
+    check(_lib.load().dp_infer_epilogue_mode(canonical.data_ptr(), SH, SW, _p(fov_deg), int(use_given),
+                                             float(f_given) if use_given else 0.0, H, W, depth.data_ptr(),
+                                             _p(f_px_out), _p(nonfinite), interp_mode(mode), _stream(depth)),
+          "dp_infer_epilogue_mode")
 
 
 def resize_u8_cv(img: torch.Tensor, out_h: int, out_w: int, area: bool) -> torch.Tensor:
@@ -372,4 +387,49 @@ def resize_u8_cv(img: torch.Tensor, out_h: int, out_w: int, area: bool) -> torch
     interp = _lib.DP_CV_INTER_AREA if area else _lib.DP_CV_INTER_LINEAR
     check(_lib.load().dp_resize_u8_cv(img.data_ptr(), H, W, out.data_ptr(), out_h, out_w, interp, _stream(out)),
           "dp_resize_u8_cv")
+    return out
+
+
+_LUTS = {}
+
+
+def colormap_lut(cmap: str, device: torch.device):
+    """(uint8 [(N + 3)][3] device table, N) of a matplotlib colormap, built from matplotlib itself
+    the way the reference's colorize_depth converts (generate_depth_maps.py:15-44): the colormap's
+    float64 RGBA at integer indices 0..N-1 (Colormap.__call__ indexes the table directly for
+    integers), under / over / bad entries, then (rgba * 255).astype(uint8)."""
+    key = (cmap, str(device))
+    if key not in _LUTS:
+        import matplotlib.pyplot as plt
+        import numpy as np
+
+        m = plt.get_cmap(cmap)
+        n = m.N
+        rgba = np.concatenate([m(np.arange(n)), m(np.array([-1.0])), m(np.array([2.0])), m(np.array([np.nan]))])
+        lut = (rgba[:, :3] * 255).astype(np.uint8)
+        _LUTS[key] = (torch.from_numpy(lut).to(device), n)
+    return _LUTS[key]
+
+
+def depth_to_image(depth: torch.Tensor, colored: bool = True, cmap: str = "turbo",
+                   out: Optional[torch.Tensor] = None, scratch: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dp_depth_to_image: the frame loop's PNG content on the GPU -- colorize_depth (uint8 HxWx3,
+    `cmap`) or the --raw uint16 HxW encoding (reference generate_depth_maps.py:15-44, 135-143),
+    byte-identical, stream-ordered (no host sync)."""
+    if depth.dtype != torch.float32 or not depth.is_contiguous():
+        raise _lib.DPError("depth_to_image expects a contiguous fp32 depth map")
+    H, W = depth.shape[-2:]
+    if scratch is None:
+        scratch = torch.empty(2, dtype=torch.int32, device=depth.device)
+    if colored:
+        lut, n = colormap_lut(cmap, depth.device)
+        if out is None:
+            out = torch.empty(H, W, 3, dtype=torch.uint8, device=depth.device)
+        mode, lp = _lib.DP_DEPTH_IMG_COLOR, lut.data_ptr()
+    else:   # uint16 bits in an int16 tensor (host: .numpy().view(np.uint16))
+        if out is None:
+            out = torch.empty(H, W, dtype=torch.int16, device=depth.device)
+        mode, lp, n = _lib.DP_DEPTH_IMG_RAW16, None, 0
+    check(_lib.load().dp_depth_to_image(depth.data_ptr(), H * W, scratch.data_ptr(), lp, n, mode, out.data_ptr(),
+                                        _stream(depth)), "dp_depth_to_image")
     return out

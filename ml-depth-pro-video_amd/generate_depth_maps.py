@@ -145,6 +145,23 @@ def _encode(depth_np: np.ndarray, output_path: str, colored: bool, cmap: str) ->
     return output_path
 
 
+def _image_async(depth: torch.Tensor, colored: bool, cmap: str) -> torch.Tensor:
+    """The PNG content of a device depth map, made on the GPU (dp_depth_to_image: colorize_depth /
+    --raw, byte-identical) and queued into pinned host memory on the current stream (no host
+    sync): the writer thread only PNG-encodes it after the frame's event."""
+    from depth_pro import ops
+
+    img = ops.depth_to_image(depth.contiguous(), colored=colored, cmap=cmap)
+    host = torch.empty(img.shape, dtype=img.dtype, pin_memory=True)
+    host.copy_(img, non_blocking=True)
+    return host
+
+
+def _host_image(host: torch.Tensor) -> np.ndarray:
+    a = host.numpy()
+    return a.view(np.uint16) if a.dtype == np.int16 else a
+
+
 def generate_depth_map(image_path, output_path=None, downscale_factor=1.0, half_precision=False, colored=True,
                        cmap="turbo"):
     """One frame (reference :46-151); returns the output path or None on error."""
@@ -158,6 +175,11 @@ def generate_depth_map(image_path, output_path=None, downscale_factor=1.0, half_
         with torch.no_grad():
             depth = model.infer(transform(image), f_px=f_px)["depth"]
         model.last_status().check()
+        if depth.is_cuda:
+            host = _image_async(depth, colored, cmap)
+            torch.cuda.current_stream(depth.device).synchronize()
+            _write_png(output_path, _host_image(host))
+            return output_path
         return _encode(depth.detach().cpu().numpy(), output_path, colored, cmap)
     except Exception as e:  # reference :147-151: report and skip the frame
         print(f"Error generating depth map for {image_path}: {str(e)}")
@@ -250,11 +272,12 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 # output), checked by the writer after the frame's event, before any file is written
                 status = model.last_status() if hasattr(model, "last_status") else None
                 pc = None
+                gpu_img = False
                 if depth.is_cuda:
-                    # queue every device->host copy behind the frame on this stream; a writer thread
-                    # waits on its event
-                    host = torch.empty(depth.shape, dtype=depth.dtype, pin_memory=True)
-                    host.copy_(depth, non_blocking=True)
+                    # the PNG content (colour / raw) made on the GPU, and every device->host copy,
+                    # queued behind the frame on this stream; a writer thread waits on its event
+                    host = _image_async(depth, colored, cmap)
+                    gpu_img = True
                     if pointcloud:
                         pc = _points(depth, pred["focallength_px"], image)
                     ev = torch.cuda.Event()
@@ -262,13 +285,17 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                 else:
                     host, ev = depth, None
 
-                def _finish(host=host, ev=ev, path=output_path, pc=pc, base=base_name, status=status):
+                def _finish(host=host, ev=ev, path=output_path, pc=pc, base=base_name, status=status,
+                            gpu_img=gpu_img):
                     if ev is not None:
                         ev.synchronize()
                     if status is not None:
                         status.check()          # raises: this frame is dropped, nothing written
                     if pc is not None:
                         PC.write_ply(os.path.join(output_dir, f"{base}_points.ply"), *_points_host(pc))
+                    if gpu_img:
+                        _write_png(path, _host_image(host))
+                        return path
                     return _encode(host.numpy(), path, colored, cmap)
 
                 pending.append(enc.submit(_finish))

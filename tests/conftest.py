@@ -17,6 +17,27 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: full-size oracle forward on the CPU (tens of seconds)")
 
 
+_METRICS = []
+
+
+@pytest.fixture
+def record(request):
+    """record(name, value): keep a measured figure (parity error, margin) of this test; written
+    as JSON to $DP_TEST_METRICS at the end of the session (DESIGN.md section 4 quotes them)."""
+    def _rec(name, value):
+        _METRICS.append({"test": request.node.nodeid, "name": name, "value": float(value)})
+    return _rec
+
+
+def pytest_sessionfinish(session, exitstatus):
+    path = os.environ.get("DP_TEST_METRICS")
+    if path and _METRICS:
+        import json
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(_METRICS, f, indent=1)
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN

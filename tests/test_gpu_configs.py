@@ -33,7 +33,7 @@ def rel_l1(a, b):
     return float(np.abs(a - b).mean() / np.abs(b).mean())
 
 
-def test_config5_frame_loop_4k_pointcloud(tmp_path, cuda, golden_dir):
+def test_config5_frame_loop_4k_pointcloud(tmp_path, cuda, golden_dir, record):
     """Two 3840x2160 frames through the drop-in loop with --raw and --pointcloud:
     depth (read back from the PLY's z, every pixel valid) vs the reference's 4K infer at
     rel-L1 < 1e-3; the PLY equals depth_to_3d(loop depth, loop f_px) bit for bit with the
@@ -71,6 +71,8 @@ def test_config5_frame_loop_4k_pointcloud(tmp_path, cuda, golden_dir):
             e_d = rel_l1(depth[::16, ::16], g["depth_sub16"])
             e_f = abs(float(pred["focallength_px"]) - float(g["f_px"])) / float(g["f_px"])
             print(f"\nconfig 5 loop, 4K frame {seed}: depth rel-L1 {e_d:.3e}, f_px rel {e_f:.2e}")
+            record("config5_loop_4k_depth_rel_l1", e_d)
+            record("config5_loop_4k_fpx_rel", e_f)
             assert e_d < 1e-3 and e_f < 1e-3
 
 
@@ -110,7 +112,7 @@ def _rank_worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_config4_nonroot_rank_builds_from_broadcast(tmp_path, golden_dir):
+def test_config4_nonroot_rank_builds_from_broadcast(tmp_path, golden_dir, record):
     """Rank 1's model comes from rank 0's broadcast packed weights (DepthPro.from_packed, device
     given as a bare 'cuda') and computes frame 0 bit for bit like rank 0's locally packed model;
     both match the reference's frame-0 forward within the parity target."""
@@ -135,7 +137,75 @@ def test_config4_nonroot_rank_builds_from_broadcast(tmp_path, golden_dir):
     d_ref = 1.0 / np.clip(g["canonical_sub8"].astype(np.float64) * (W / f_ref), 1e-4, 1e4)
     e = rel_l1(d1[::8, ::8], d_ref)
     print(f"\nconfig 4 rank 1 (from_packed) frame 0 depth rel-L1 {e:.3e}")
+    record("config4_rank1_depth_rel_l1", e)
     assert e < 1e-3
+
+
+def _nccl_worker(port, outdir):
+    """World-1 process group over the nccl backend (RCCL) on cuda:0: every collective the frame-
+    parallel paths use runs through RCCL once (bench.py, distributed.py, generate_depth_maps)."""
+    import torch.distributed as dist
+
+    import depth_pro
+    from depth_pro import distributed as D
+    from depth_pro.depth_pro import DepthPro
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DEPTH_PRO_SYNTHETIC="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    res = {}
+    try:
+        assert dist.get_backend() == "nccl"
+        cfg = depth_pro.depth_pro.run_config()
+        # create_model_and_transforms_shared: broadcast_object_list + the one-blob weight broadcast
+        model, transform = D.create_model_and_transforms_shared(cfg, torch.device("cuda"), torch.float32)
+        # the non-root path: an engine built on the RCCL-broadcast blob (DepthPro.from_packed)
+        received = D.broadcast_packed(model.engine().P, dev, src=0)
+        other = DepthPro.from_packed(received, dev, model.compute_dtype, use_fov_head=model.use_fov_head)
+        x = transform(frame(0))
+        with torch.no_grad():
+            d_local = model.infer(x)["depth"].clone()
+            d_recv = other.infer(x)["depth"].clone()
+        model.last_status().check()
+        other.last_status().check()
+        res["equal"] = bool(torch.equal(d_local, d_recv))
+        # the per-step depth gather: gather_frames (async handle) and the raw RCCL gather under it
+        bufs, work = D.gather_frames(d_recv, dst=0, async_op=True)
+        if work is not None:
+            work.wait()
+        gl = [torch.empty_like(d_recv)]
+        w2 = dist.gather(d_recv, gather_list=gl, dst=0, async_op=True)
+        w2.wait()
+        torch.cuda.synchronize()
+        res["gather_equal"] = bool(torch.equal(bufs[0], d_local) and torch.equal(gl[0], d_local))
+        # bench.py's max-over-ranks timing
+        t = torch.tensor([1.25], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        res["allreduce"] = float(t.item())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+    import json
+    with open(os.path.join(outdir, "nccl.json"), "w") as f:
+        json.dump(res, f)
+
+
+def test_config4_collectives_over_rccl(tmp_path):
+    """the RCCL (nccl-backend) code of the frame-parallel path executes on
+    the GPU box: weight broadcast, engine from the broadcast blob bit-identical to the local one,
+    the depth gather and the max-over-ranks all-reduce (world 1: one GPU per box)."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), str(tmp_path)))
+    p.start()
+    p.join(600)
+    assert p.exitcode == 0
+    res = json.loads((tmp_path / "nccl.json").read_text())
+    assert res == {"equal": True, "gather_equal": True, "allreduce": 1.25}, res
 
 
 def test_frame_loop_drops_exactly_the_failed_frame(tmp_path, cuda):
@@ -205,7 +275,7 @@ def test_frame_loop_downscale_factor(tmp_path, cuda, factor):
     assert np.array_equal(png, G.colorize_depth(depth))
 
 
-def test_stressed_weights_mixed_precision_margin(cuda, golden_dir):
+def test_stressed_weights_mixed_precision_margin(cuda, golden_dir, record):
     """Parity outside the benign synthetic distribution (LayerScale x5 and outlier residual
     channels, depth_pro.weights.stressed_state_dict; reference forward: golden_stress_frame0.npz)
     in the default mixed mode (bf16 ViTs, f16 decoder): every output finite (no f16 overflow in
@@ -236,4 +306,7 @@ def test_stressed_weights_mixed_precision_margin(cuda, golden_dir):
     e_f = abs(fov.item() - float(g["fov_deg"][0])) / abs(float(g["fov_deg"][0]))
     print(f"\nstressed weights (mixed): canonical rel-L1 {e_c:.3e}  depth rel-L1 {e_d:.3e}  fov rel {e_f:.2e}; "
           f"reference residual |max| {g['residual_absmax']}, decoder features |max| {float(g['features_absmax']):.1f}")
+    record("stress_mixed_canonical_rel_l1", e_c)
+    record("stress_mixed_depth_rel_l1", e_d)
+    record("stress_mixed_fov_rel", e_f)
     assert e_d < 1e-3 and e_f < 1e-3

@@ -355,6 +355,58 @@ def test_resize_and_infer_epilogue(cuda, HW):
                                rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("HW", [(1536, 1536), (1080, 1920), (500, 333), (3000, 2000)])
+def test_resize_and_infer_epilogue_bicubic(cuda, HW):
+    """interpolation_mode="bicubic" (reference depth_pro.py:273-291 passes it to both
+    F.interpolate calls): dp_resize / dp_infer_epilogue_mode vs torch's upsample_bicubic2d
+    (align_corners=False, A = -0.75, clamped border taps) in fp32 on the CPU."""
+    H, W = HW
+    g = torch.Generator().manual_seed(H + 7)
+    x = torch.randn(3, H, W, generator=g)
+    out = torch.empty(3, 1536, 1536, device=cuda)
+    ops.resize(x.to(cuda), out, "bicubic")
+    ref = F.interpolate(x[None], size=(1536, 1536), mode="bicubic", align_corners=False)[0]
+    assert (out.cpu() - ref).abs().max() < 2e-5
+    canon = torch.rand(1, 1, 1536, 1536, generator=g) * 3 + 0.01
+    fov = torch.tensor([[[[61.0]]]])
+    depth = torch.empty(H, W, device=cuda)
+    fpx = torch.empty((), device=cuda)
+    ops.infer_epilogue(canon.to(cuda), fov.to(cuda), None, H, W, depth, fpx, mode="bicubic")
+    f_ref = 0.5 * W / torch.tan(0.5 * torch.deg2rad(fov.float()))
+    inv = canon * (W / f_ref)
+    if (H, W) != (1536, 1536):
+        inv = F.interpolate(inv, size=(H, W), mode="bicubic", align_corners=False)
+    dref = 1.0 / torch.clamp(inv, 1e-4, 1e4)
+    np.testing.assert_allclose(depth.cpu().numpy(), dref[0, 0].numpy(), rtol=5e-5, atol=1e-6)
+    with pytest.raises(ValueError):
+        ops.resize(x.to(cuda), out, "nearest")
+
+
+@pytest.mark.parametrize("case", ["random", "nan", "const", "4k", "viridis"])
+def test_depth_to_image_matches_reference_writers(cuda, case):
+    """dp_depth_to_image == the reference writers byte for byte: colorize_depth (matplotlib
+    turbo over the per-frame nanmin / nanmax, generate_depth_maps.py:15-44) and the --raw uint16
+    encoding (:135-143), incl. NaN pixels and a constant map (0/0 -> matplotlib's bad colour)."""
+    import generate_depth_maps as G
+
+    rng = np.random.default_rng(len(case))
+    H, W = (2160, 3840) if case == "4k" else (333, 517)
+    d = (rng.random((H, W), dtype=np.float32) * 30 + 0.05).astype(np.float32)
+    if case == "nan":
+        d[rng.random((H, W)) < 0.01] = np.nan
+    if case == "const":
+        d[:] = 7.25
+    cmap = "viridis" if case == "viridis" else "turbo"
+    dev = torch.from_numpy(d).to(cuda)
+    col = ops.depth_to_image(dev, colored=True, cmap=cmap).cpu().numpy()
+    raw = ops.depth_to_image(dev, colored=False).cpu().numpy().view(np.uint16)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        ref_col = G.colorize_depth(d, cmap=cmap)
+        ref_raw = G.raw_depth_u16(d)
+    assert np.array_equal(col, ref_col), (col != ref_col).sum()
+    assert np.array_equal(raw, ref_raw), (raw != ref_raw).sum()
+
+
 def test_normalize_u8(cuda):
     img = np.random.default_rng(0).integers(0, 256, (300, 200, 3), dtype=np.uint8)
     out = torch.empty(3, 300, 200, device=cuda)

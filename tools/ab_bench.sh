@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 for R in 1 2; do
   for F in "$@"; do
-    DP_GEMM_DEBUG=$F timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $OUT/ab_${F}_$R.json 2> $OUT/ab_${F}_$R.err
+    DP_GEMM_DEBUG=$F timeout -k 10 300 python -u bench.py --ab --no-cpu-baseline --steps 40 > $OUT/ab_${F}_$R.json 2> $OUT/ab_${F}_$R.err
   done
 done
 python - "$OUT" <<'PY'
@@ -15,5 +15,5 @@ import json, sys, glob
 for f in sorted(glob.glob(sys.argv[1] + "/ab_*.json")):
     d = json.load(open(f))
     dk = d["roofline"]["dominant_kernel"]
-    print(f.split("/")[-1], d["value"], d["ms_per_step"], d["parity"]["depth_rel_l1"], dk["engine"]["tile"], dk["avg_us"])
+    print(f.split("/")[-1], d["ab_fps"], d["ms_per_step"], d["parity"]["depth_rel_l1"], dk["engine"]["tile"], dk["avg_us"])
 PY

@@ -14,7 +14,7 @@ mkdir -p $OUT
 for S in $STEPS; do
   case $S in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+      DP_TEST_METRICS=$OUT/test_metrics.json timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread \
         > $OUT/pytest_gpu.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > $OUT/smoke.log 2>&1 ;;
@@ -51,8 +51,12 @@ for S in $STEPS; do
         > $OUT/gemm_fc1_engines.txt 2>&1 ;;
     side)
       # side-encoder cost by ablation (DP_ABLATE=side: image / FOV encoders skipped) vs the full frame
-      DP_ABLATE=side timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $OUT/bench_noside.json 2> $OUT/bench_noside.err
+      DP_ABLATE=side timeout -k 10 300 python -u bench.py --ab --no-cpu-baseline --steps 40 > $OUT/bench_noside.json 2> $OUT/bench_noside.err
       timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $OUT/bench_side.json 2> $OUT/bench_side.err ;;
+    loop)
+      # the video loop as users run it (configs 3 and 5): PNG frames -> GPU -> PNG (+ PLY)
+      timeout -k 10 400 python -u tools/loop_bench.py --frames 64 --size 1536x1536 > $OUT/loop_1536.log 2>&1
+      timeout -k 10 400 python -u tools/loop_bench.py --frames 8 --size 3840x2160 --pointcloud > $OUT/loop_4k_pc.log 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
   echo "step $S ok"
