@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 9
+#define DP_ABI_VERSION 10
 int dp_abi_version(void);
 
 /*
@@ -121,6 +121,23 @@ typedef struct dp_gemm_args {
                                the caller for THIS stream (never shared by concurrent launches);
                                enables the persistent stream-K engine for large 256x256-tiled GEMMs */
   int64_t workspace_bytes;
+  /* LayerNorm folded across the GEMM boundary (timm Block norm1 / norm2, eps ln_eps), dense A,
+   * the 8-phase 320 x 256 engine (DP_TILE_8PH_320x256; NULL fields: off):
+   *  producer -- the residual GEMM (accumulate into fp32 C, act none) also writes
+   *    ln_xb_out:   the new rows of C in 16 bits (dtype), [M][ldc];
+   *    ln_part_out: fp32 [M][N/128][2]: (mean, M2) of each 128-column chunk of the new rows;
+   *  consumer -- A = a producer's ln_xb_out (un-normalised rows), B = W o ln.weight (per k)
+   *    [o gamma (per n)], bias = (b + W . ln.bias) [* gamma], gamma = NULL,
+   *    ln_part_in = the producer's ln_part_out ([M][K/128][2]), ln_colsum[N] = sum_k B[n][k]
+   *    (the 16-bit values, summed exactly); the epilogue's value before act is
+   *      v = rstd * acc - rstd * mean * ln_colsum[n] + bias[n]
+   *    with (mean, rstd) of the row merged from its K/128 chunks: LN(x) . W^T + b exactly, up
+   *    to where the 16-bit rounding falls (x instead of LN(x)). */
+  float* ln_part_out;
+  void* ln_xb_out;
+  const float* ln_part_in;
+  const float* ln_colsum;
+  float ln_eps;
 } dp_gemm_args;
 
 enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32 = 3,
@@ -191,6 +208,16 @@ int dp_gemm_plan(const dp_gemm_args* args, int32_t* tile, int32_t* grid);
  */
 int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy,
                  int32_t rows, int32_t cols, float eps, int32_t dtype, dp_stream_t stream);
+
+/*
+ * dp_layernorm_stats: the input side of a folded LayerNorm (dp_gemm_args.ln_*): for the rows of
+ * fp32 x [rows][cols] (cols % 128 == 0, <= 2048) write x in 16 bits (xb [rows][ldxb], dtype) and
+ * part fp32 [rows][cols/128][2] = (mean, M2) of each 128-column chunk -- what the residual GEMMs'
+ * producer epilogue writes, for the rows no GEMM produced (the patch embed + cls rows that enter
+ * ViT block 0).
+ */
+int dp_layernorm_stats(const float* x, int64_t ldx, int32_t rows, int32_t cols, void* xb, int64_t ldxb,
+                       float* part, int32_t dtype, dp_stream_t stream);
 
 /*
  * dp_layernorm_grouped: dp_layernorm over groups * rows_per_group rows, rows of group g taking

@@ -106,6 +106,18 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
         a->M % (a->dc_h * a->dc_w) != 0)
       return DP_ERR_SHAPE;
   }
+  // folded LayerNorm (ln_*): the 8-phase 320 x 256 engine only, producer = the fp32 residual
+  // accumulate without activation (N % 128 == 0), consumer = 16-bit C over K = 1024 rows whose
+  // gamma is folded into B / bias
+  const bool lnp = a->ln_part_out || a->ln_xb_out, lnc = a->ln_part_in || a->ln_colsum;
+  if (lnp && lnc) return DP_ERR_ARG;
+  if (lnp && (!a->ln_part_out || !a->ln_xb_out || !a->accumulate || a->c_dtype != DP_F32 || a->act != DP_ACT_NONE ||
+              a->N % 128 != 0))
+    return DP_ERR_ARG;
+  if (lnc && (!a->ln_part_in || !a->ln_colsum || a->K != 1024 || a->accumulate || a->c_dtype == DP_F32 ||
+              a->gamma || (a->act != DP_ACT_NONE && a->act != DP_ACT_GELU) || !(a->ln_eps > 0.f)))
+    return DP_ERR_ARG;
+  if ((lnp || lnc) && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_8PH_320x256) return DP_ERR_ARG;
   const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
   const int dbg = g_dbg_flags.load(std::memory_order_relaxed);
   tile = a->tile;
@@ -236,6 +248,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // (load-free with a 16-bit C, or the fp32 residual accumulate without activation) -- the
   // planner's dense 320 x 256 launches (ViT qkv / proj / fc2) run on it (qkv 130.6 -> 115.8,
   // fc2 149.6 -> 142.0 us, profiles/r03d_8ph320; debug 1 << 15: off)
+  if (lnp || lnc) tile = DP_TILE_8PH_320x256;   // the engine with the folded-LN epilogues
   if (tile == DP_TILE_8PH_320x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_BIG_320x256 && !(dbg & (1 << 15)))) {
     const bool plain = a->a_mode == DP_A_DENSE && !a->relu_a && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
                        !a->R1 && !a->R2 && !a->pos && !a->row_group && !a->head_w && !a->head_corr &&
@@ -273,6 +286,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.store_mode = a->store_mode; p.dc_h = a->dc_h; p.dc_w = a->dc_w; p.dc_cout = a->dc_cout;
   p.row_group = a->row_group; p.row_group_out = a->row_group_out; p.row_off = a->row_off;
   p.head_w = a->head_w; p.head_b = a->head_b; p.head_corr = a->head_corr;
+  p.ln_part_out = a->ln_part_out; p.ln_xb_out = (u16*)a->ln_xb_out;
+  p.ln_part_in = a->ln_part_in; p.ln_colsum = a->ln_colsum; p.ln_eps = a->ln_eps;
   p.tiles_n = 1;
   p.tiles_m = 1;
   if (tile == DP_TILE_STREAMK_256x256) {
@@ -347,7 +362,8 @@ extern "C" int dp_gemm_grouped(const dp_gemm_args* a, int32_t groups, dp_stream_
         !y.R2 != !x.R2 || y.ldr2 != x.ldr2 || y.ldc != x.ldc || y.c_dtype != x.c_dtype ||
         y.accumulate != x.accumulate || y.store_mode != DP_STORE_ROWS || x.store_mode != DP_STORE_ROWS ||
         y.row_group != x.row_group || y.row_group_out != x.row_group_out || y.row_off != x.row_off ||
-        y.head_w || y.head_corr || y.N % 8 != 0)
+        y.head_w || y.head_corr || y.N % 8 != 0 || y.ln_part_out || y.ln_xb_out || y.ln_part_in ||
+        y.ln_colsum)
       return DP_ERR_ARG;
     if (g == 0) p = q;
     p.grp[g] = GemmP::Group{q.A, q.B, q.bias, q.gamma, q.pos, q.R1, q.R2, q.C};

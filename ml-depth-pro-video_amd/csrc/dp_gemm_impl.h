@@ -70,6 +70,12 @@ struct GemmP {
   int stagger_wg, stagger_sleeps;   // 2-workgroup-per-CU engine: start stagger (debug 1 << 21)
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
   unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
+  // LayerNorm folded across the GEMM boundary (dp_gemm_args.ln_*; the 8-phase 320 x 256 engine)
+  float* ln_part_out;      // producer: (mean, M2) per 128-column chunk of the new C rows
+  u16* ln_xb_out;          // producer: the new C rows in 16 bits ([M][ldc])
+  const float* ln_part_in; // consumer: the A rows' chunk statistics ([M][K/128][2])
+  const float* ln_colsum;  // consumer: sum_k B[n][k]
+  float ln_eps;
   // dp_gemm_grouped: `groups` problems of one shape in one launch (workgroup range g * tiles_m *
   // tiles_n ... covers problem g, whose operand pointers are grp[g]); 1 otherwise
   int groups;
@@ -520,6 +526,100 @@ __device__ __forceinline__ void epilogue_rows_buf(const GemmP& p, const ColConst
   }
 }
 
+// epilogue_acc32_wide + the producer side of a folded LayerNorm: besides C (fp32, accumulated),
+// the new rows go out in 16 bits (p.ln_xb_out, staged through the wave's LDS region so each row
+// leaves as one 256-B segment) and, per row, (mean, M2) of the wave's 128 columns
+// (p.ln_part_out[m][n_base / 128]) -- shifted single-pass sums (shift = the row's first value,
+// so no cancellation) reduced over the row's 4 lanes.  C is bit-identical to epilogue_acc32_wide.
+// `slab`: the wave's LDS region, >= 5 KiB.
+template <typename K_, int FM, int FN>
+__device__ __forceinline__ void epilogue_acc32_wide_ln(const GemmP& p, f32x4_t (&acc)[FM][FN], char* slab, int lane,
+                                                       int m_base, int n_base) {
+  #pragma clang fp contract(off)
+  static_assert(FN == 8, "wide epilogue");
+  constexpr int H = FN / 2;
+  const int t = lane & 15, g = lane >> 4;
+  {
+    const int c = 4 * (lane & 31), n = n_base + c;
+    f32x4_t v;
+    if (lane < 32) v = (p.bias && n < p.N) ? *(const f32x4_t*)(p.bias + n) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    else v = (p.gamma && n < p.N) ? *(const f32x4_t*)(p.gamma + n) : f32x4_t{1.f, 1.f, 1.f, 1.f};
+    *(f32x4_t*)(slab + (lane < 32 ? 0 : 512) + c * 4) = v;
+  }
+  char* const xst = slab + 1024;          // 16 rows x 128 columns x 16 bit, chunk ^ row swizzle
+  float* const C = (float*)p.C;
+  const int nch = p.N / 128;
+  f32x4_t cur[H], nxt[H];
+  auto load = [&](int ch, f32x4_t (&c)[H]) __attribute__((always_inline)) {
+    const int fm = ch >> 1, h = ch & 1;
+    const int m = min(m_base + fm * 16 + t, p.M - 1);
+    #pragma unroll
+    for (int f = 0; f < H; ++f)
+      c[f] = *(const f32x4_t*)(C + (long long)m * p.ldc + n_base + (h * H + f) * 16 + 4 * g);
+  };
+  load(0, cur);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float sh = 0.f, s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+  for (int ch = 0; ch < 2 * FM; ++ch) {
+    if (ch + 1 < 2 * FM) load(ch + 1, nxt);
+    const int fm = ch >> 1, h = ch & 1;
+    const int m = m_base + fm * 16 + t;
+    #pragma unroll
+    for (int f = 0; f < H; ++f) {
+      const int fn = h * H + f;
+      const f32x4_t b = *(const f32x4_t*)(slab + (fn * 16 + 4 * g) * 4);
+      const f32x4_t q = *(const f32x4_t*)(slab + 512 + (fn * 16 + 4 * g) * 4);
+      f32x4_t x;
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[fm][fn][r] + b[r];
+        x[r] = v * q[r] + cur[f][r];
+      }
+      if (m < p.M) *(f32x4_t*)(C + (long long)m * p.ldc + n_base + fn * 16 + 4 * g) = x;
+      if (h == 0 && f == 0) {
+        sh = __shfl(x[0], t);             // the row's value at column n_base (lane t, g = 0)
+        s1 = 0.f;
+        s2 = 0.f;
+      }
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = x[r] - sh;
+        s1 += d;
+        s2 += d * d;
+      }
+      uint2 w;
+      w.x = K_::pack2(x[0], x[1]);
+      w.y = K_::pack2(x[2], x[3]);
+      *(uint2*)(xst + t * 256 + (((fn * 2 + (g >> 1)) ^ t) << 4) + (g & 1) * 8) = w;
+    }
+    #pragma unroll
+    for (int f = 0; f < H; ++f) cur[f] = nxt[f];
+    if (h == 1) {
+      // the row's 128 columns: 4 lanes (g) of 32 values each
+      s1 += __shfl_xor(s1, 16);
+      s2 += __shfl_xor(s2, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      if (g == 0 && m < p.M) {
+        const float mc = sh + s1 * (1.f / 128);
+        const float m2 = s2 - s1 * (s1 * (1.f / 128));
+        *(float2*)(p.ln_part_out + ((long long)m * nch + n_base / 128) * 2) = make_float2(mc, m2);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's staging writes
+      #pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int row = k * 4 + (lane >> 4), chunk = lane & 15;
+        const uint4 d = *(const uint4*)(xst + row * 256 + ((chunk ^ row) << 4));
+        const int mm = m_base + fm * 16 + row;
+        if (mm < p.M) *(uint4*)(p.ln_xb_out + (long long)mm * p.ldc + n_base + chunk * 8) = d;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read back before the next row's writes
+    }
+  }
+}
+
+
 // Epilogue variants.  needs_rowld: the launch reads per-row operands (R1 / R2, pos, the fp32 C
 // it accumulates into) or stores through a remap (deconv pixel shuffle, row groups, the fused /
 // composed heads).  Without any of those (and with a 16-bit C) the engines take the load-free
@@ -586,6 +686,81 @@ __device__ __forceinline__ void epilogue_mfma(const GemmP& p, f32x4_t (&acc)[FM]
       const int m = m_base + f0 * 16 + row, n = n_base + chunk * 8;
       if (m < p.M && n < p.N) *(uint4*)((u16*)p.C + (long long)m * p.ldc + n) = d;
     }
+  }
+}
+
+// epilogue_mfma for the consumer of a folded LayerNorm (the ViT qkv / fc1 over un-normalised
+// 16-bit rows, dp_gemm_args.ln_part_in): per value v = rstd * acc - rstd * mean * colsum[n] +
+// bias[n], then ACT, packed to 16 bits and stored as epilogue_mfma does (PF = 1).  The wave's
+// bias / colsum live in its LDS region (first KiB; staging after it), and each fragment row's
+// 8 chunk statistics are loaded one row ahead and merged (Chan) -- no per-column or per-row
+// register arrays beside the 160 accumulators.  `slab` >= 1 KiB + 16 * TN * 2 bytes.
+template <typename K_, int ACT, int FM, int FN, int TN>
+__device__ __forceinline__ void epilogue_mfma_lnc(const GemmP& p, f32x4_t (&acc)[FM][FN], char* slab, int lane,
+                                                  int m_base, int n_base) {
+  constexpr int CH = TN / 8, RPI = 64 / CH;
+  static_assert(TN == 128 && FN == 8, "wide consumer epilogue");
+  const int t = lane & 15, g = lane >> 4;
+  {
+    // lanes 0-31: bias of columns 4 lane .. +3; lanes 32-63: colsum
+    const int c = 4 * (lane & 31), n = n_base + c;
+    f32x4_t v;
+    if (lane < 32) v = (p.bias && n < p.N) ? *(const f32x4_t*)(p.bias + n) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    else v = n < p.N ? *(const f32x4_t*)(p.ln_colsum + n) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    *(f32x4_t*)(slab + (lane < 32 ? 0 : 512) + c * 4) = v;
+  }
+  char* const stg = slab + 1024;
+  f32x4_t cur[4], nxt[4];
+  auto load = [&](int fm, f32x4_t (&c)[4]) __attribute__((always_inline)) {
+    const int m = min(m_base + fm * 16 + t, p.M - 1);
+    const f32x4_t* pp = (const f32x4_t*)(p.ln_part_in + (long long)m * 16);
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = pp[i];
+  };
+  load(0, cur);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the constants, before any read of them
+  #pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    if (fm + 1 < FM) load(fm + 1, nxt);
+    // the row's mean / rstd from its 8 chunks of 128 columns
+    const float mean = (((cur[0][0] + cur[0][2]) + (cur[1][0] + cur[1][2])) +
+                        ((cur[2][0] + cur[2][2]) + (cur[3][0] + cur[3][2]))) * (1.f / 8);
+    float m2 = 0.f;
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d0 = cur[i][0] - mean, d1 = cur[i][2] - mean;
+      m2 += (cur[i][1] + 128.f * d0 * d0) + (cur[i][3] + 128.f * d1 * d1);
+    }
+    const float rs = rsqrtf(m2 * (1.f / 1024) + p.ln_eps), nm = -rs * mean;
+    #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const f32x4_t b = *(const f32x4_t*)(slab + (fn * 16 + 4 * g) * 4);
+      const f32x4_t q = *(const f32x4_t*)(slab + 512 + (fn * 16 + 4 * g) * 4);
+      f32x4_t x = __builtin_elementwise_fma(acc[fm][fn], (f32x4_t)(rs), __builtin_elementwise_fma(q, (f32x4_t)(nm), b));
+      if constexpr (ACT == DP_ACT_RELU) {
+        #pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = fmaxf(x[r], 0.f);
+      } else if constexpr (ACT == DP_ACT_GELU) {
+        x = gelu_erf4(x);
+      }
+      const int row = t;
+      const int chunk = fn * 2 + (g >> 1);
+      uint2 w;
+      w.x = K_::pack2(x[0], x[1]);
+      w.y = K_::pack2(x[2], x[3]);
+      *(uint2*)(stg + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4) + (g & 1) * 8) = w;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    #pragma unroll
+    for (int k = 0; k < 16 / RPI; ++k) {
+      const int row = k * RPI + lane / CH, chunk = lane % CH;
+      const uint4 d = *(const uint4*)(stg + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4));
+      const int m = m_base + fm * 16 + row, n = n_base + chunk * 8;
+      if (m < p.M && n < p.N) *(uint4*)((u16*)p.C + (long long)m * p.ldc + n) = d;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    #pragma unroll
+    for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
   }
 }
 // Residual-accumulate epilogue in the MFMA register layout (fp32 C += (acc + bias) act * gamma,
@@ -1949,7 +2124,7 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
 // s+1 in phase 3 -- so each piece has 4+ phases to land and the count is 8 in steady state.
 // Dense A only; epilogues: the load-free MFMA-layout one (EACT = DP_ACT_*; 16-bit C) or the
 // fp32 residual-accumulate one (EACT = EPI_ACC + act).
-template <typename K_, int EACT>
+template <typename K_, int EACT, int LNM = 0>   // LNM: 1 folded-LN producer, 2 consumer
 __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   constexpr int BM = 320;
   constexpr int A_BYTES = BM * 128, B_BYTES = 256 * 128, BUF = A_BYTES + B_BYTES;
@@ -2075,8 +2250,12 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
     return;
   }
   lds_barrier();   // the ring is free once every wave has left the K loop
-  if constexpr (EACT >= EPI_ACC)
+  if constexpr (LNM == 1)
+    epilogue_acc32_wide_ln<K_, FM, FN>(p, acc, smem + wave * 8192, lane, m0 + wm * TM, n0 + wn * TN);
+  else if constexpr (EACT >= EPI_ACC)
     epilogue_acc32_wide<EACT - EPI_ACC, FM, FN>(p, acc, smem + wave * SLAB, lane, m0 + wm * TM, n0 + wn * TN);
+  else if constexpr (LNM == 2)
+    epilogue_mfma_lnc<K_, EACT, FM, FN, TN>(p, acc, smem + wave * 8192, lane, m0 + wm * TM, n0 + wn * TN);
   else
     epilogue_mfma<K_, EACT, FM, FN, TN, PF>(p, acc, smem + wave * SLAB, lane, m0 + wm * TM, n0 + wn * TN);
 }
@@ -2089,6 +2268,21 @@ int launch_8ph320(const GemmP& p0, hipStream_t s) {
   const int ea = fast_epi_act(p);
   if (p.N % 256 || ea < 0 || p.relu_a) return DP_ERR_ARG;
   dim3 grid(p.tiles_n * p.tiles_m);
+  if (p.ln_part_out) {   // folded-LN producer: the residual accumulate
+    if (ea != EPI_ACC + DP_ACT_NONE || !p.ln_xb_out) return DP_ERR_ARG;
+    hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 1>), grid, dim3(512), 0, s, p);
+    DP_CHECK_LAUNCH();
+    return 0;
+  }
+  if (p.ln_part_in) {    // folded-LN consumer (qkv / fc1): 16-bit C, K = 1024
+    switch (ea) {
+      case DP_ACT_NONE: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, DP_ACT_NONE, 2>), grid, dim3(512), 0, s, p); break;
+      case DP_ACT_GELU: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, DP_ACT_GELU, 2>), grid, dim3(512), 0, s, p); break;
+      default: return DP_ERR_ARG;
+    }
+    DP_CHECK_LAUNCH();
+    return 0;
+  }
   switch (ea) {
     case DP_ACT_NONE: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, DP_ACT_NONE>), grid, dim3(512), 0, s, p); break;
     case DP_ACT_RELU: hipLaunchKernelGGL((gemm_8ph320_kernel<K_, DP_ACT_RELU>), grid, dim3(512), 0, s, p); break;

@@ -118,6 +118,42 @@ int ln_launch(const float* x, long long ldx, const LnW& lw, u16* y, long long ld
   return 0;
 }
 
+// The input side of a folded LayerNorm (dp_layernorm_stats): one wave per row, lane l owns the 8
+// columns 8 l + 512 j (as ln_kernel); each 128-column chunk is 16 lanes.  Writes the row in 16
+// bits and the chunk's (mean, M2), two-pass within the chunk (fp32), the same statistics the
+// residual GEMMs' producer epilogue writes for the rows it makes (dp_gemm_args.ln_part_out).
+template <typename K_, int VEC>
+__global__ void __launch_bounds__(256) ln_stats_kernel(const float* __restrict__ x, long long ldx, int rows,
+                                                       u16* __restrict__ xb, long long ldxb, float* __restrict__ part) {
+  constexpr int G = VEC / 2, COLS = VEC * 256, NCH = COLS / 128;
+  const int lane = threadIdx.x & 63;
+  const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * ldx;
+  #pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const float4 a = *(const float4*)(xr + j * 512 + lane * 8);
+    const float4 b = *(const float4*)(xr + j * 512 + lane * 8 + 4);
+    float s = (a.x + a.y) + (a.z + a.w) + ((b.x + b.y) + (b.z + b.w));
+    #pragma unroll
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o);
+    const float mean = s * (1.f / 128);
+    const float d0 = a.x - mean, d1 = a.y - mean, d2 = a.z - mean, d3 = a.w - mean;
+    const float d4 = b.x - mean, d5 = b.y - mean, d6 = b.z - mean, d7 = b.w - mean;
+    float q = (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3) + ((d4 * d4 + d5 * d5) + (d6 * d6 + d7 * d7));
+    #pragma unroll
+    for (int o = 1; o < 16; o <<= 1) q += __shfl_xor(q, o);
+    uint4 w;
+    w.x = K_::pack2(a.x, a.y); w.y = K_::pack2(a.z, a.w);
+    w.z = K_::pack2(b.x, b.y); w.w = K_::pack2(b.z, b.w);
+    *(uint4*)(xb + (long long)row * ldxb + j * 512 + lane * 8) = w;
+    if ((lane & 15) == 0) {
+      const int ch = j * 4 + (lane >> 4);
+      *(float2*)(part + ((long long)row * NCH + ch) * 2) = make_float2(mean, q);
+    }
+  }
+}
+
 // --------------------------------------------------------- u8 HWC -> CHW norm
 template <int OUT>
 __global__ void normalize_kernel(const uint8_t* __restrict__ img, int HW, void* __restrict__ out) {
@@ -488,6 +524,27 @@ inline int blocks_for(long long n, int bs) { return (int)((n + bs - 1) / bs); }
 }  // namespace
 
 extern "C" int dp_abi_version(void) { return DP_ABI_VERSION; }
+
+extern "C" int dp_layernorm_stats(const float* x, int64_t ldx, int32_t rows, int32_t cols, void* xb, int64_t ldxb,
+                                  float* part, int32_t dtype, dp_stream_t stream) {
+  if (!x || !xb || !part) return DP_ERR_ARG;
+  if (rows <= 0 || ldx % 4 || ldxb % 8) return DP_ERR_ALIGN;
+  dim3 grid((rows + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+#define DP_LS(V_) do { \
+    if (dtype == DP_BF16) hipLaunchKernelGGL((ln_stats_kernel<KBF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, part); \
+    else if (dtype == DP_F16) hipLaunchKernelGGL((ln_stats_kernel<KF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, part); \
+    else return DP_ERR_DTYPE; } while (0)
+  switch (cols) {
+    case 512: DP_LS(2); break;
+    case 1024: DP_LS(4); break;
+    case 2048: DP_LS(8); break;
+    default: return DP_ERR_SHAPE;
+  }
+#undef DP_LS
+  DP_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy,
                             int32_t rows, int32_t cols, float eps, int32_t dtype, dp_stream_t stream) {

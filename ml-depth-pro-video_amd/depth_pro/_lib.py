@@ -26,7 +26,7 @@ INTERP_MODES = {"bilinear": DP_INTERP_BILINEAR, "bicubic": DP_INTERP_BICUBIC}
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
  DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128,
  DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256) = range(21)
-DP_ABI_VERSION = 9
+DP_ABI_VERSION = 10
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -36,7 +36,7 @@ LIB_PATH = os.environ.get(
 
 # (name, ctypes type) in header order
 EXPORTS = (
-    "dp_abi_version", "dp_gemm", "dp_gemm_grouped", "dp_layernorm", "dp_layernorm_grouped", "dp_attention",
+    "dp_abi_version", "dp_gemm", "dp_gemm_grouped", "dp_layernorm", "dp_layernorm_grouped", "dp_layernorm_stats", "dp_attention",
     "dp_attention_log2q", "dp_normalize_u8",
     "dp_resize_bilinear", "dp_resize", "dp_patchify_pyramid", "dp_vit_cls_rows", "dp_merge_windows",
     "dp_merge_windows_range", "dp_fov_tail", "dp_infer_epilogue", "dp_infer_epilogue_mode", "dp_gemm_workspace_size", "dp_gemm_plan",
@@ -70,6 +70,8 @@ class GemmArgs(ctypes.Structure):
         ("head_w", ctypes.c_void_p), ("head_b", ctypes.c_float), ("head_corr", ctypes.c_void_p),
         ("tile", ctypes.c_int32),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
+        ("ln_part_out", ctypes.c_void_p), ("ln_xb_out", ctypes.c_void_p), ("ln_part_in", ctypes.c_void_p),
+        ("ln_colsum", ctypes.c_void_p), ("ln_eps", ctypes.c_float),
     ]
 
 
@@ -102,6 +104,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "dp_gemm_grouped": [ctypes.POINTER(GemmArgs), i32, vp],
         "dp_layernorm_grouped": [vp, i64, vp, vp, i32, vp, i64, i32, i32, f32, i32, vp],
         "dp_layernorm": [vp, i64, vp, vp, vp, i64, i32, i32, f32, i32, vp],
+        "dp_layernorm_stats": [vp, i64, i32, i32, vp, i64, vp, i32, vp],
         "dp_attention": [vp, vp, i32, i32, i32, i32, f32, i32, vp],
         "dp_attention_log2q": [vp, vp, i32, i32, i32, i32, i32, vp],
         "dp_normalize_u8": [vp, i32, i32, vp, i32, vp],

@@ -152,6 +152,19 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code) 
                 P[b + n] = g(b + n).to(vdt).contiguous()
         P[vit + "norm.weight"] = _f32(g(vit + "norm.weight"))
         P[vit + "norm.bias"] = _f32(g(vit + "norm.bias"))
+        if vit == "encoder.patch_encoder.":
+            # norm1 / norm2 folded into the qkv / fc1 that consume them (ops.fold_layernorm): the
+            # patch encoder's residual GEMMs hand the next Linear 16-bit rows + chunk statistics
+            # instead of a LayerNorm pass (Engine._vit); the qkv's log2q gamma rides
+            # in the folded weights
+            qg = ops.log2q_gamma(HEADS, D // HEADS, device)
+            for i in range(DEPTH):
+                b = f"{vit}blocks.{i}."
+                for lin, ln, cs in (("attn.qkv", "norm1", qg), ("mlp.fc1", "norm2", None)):
+                    wf, bf, sf = ops.fold_layernorm(g(b + lin + ".weight").float(), g(b + lin + ".bias").float(),
+                                                    g(b + ln + ".weight").float(), g(b + ln + ".bias").float(),
+                                                    vdt, cs)
+                    P[b + lin + ".fold.w"], P[b + lin + ".fold.b"], P[b + lin + ".fold.s"] = wf, bf, sf
     # encoder project / upsample
     for name, n_up in (("upsample_latent0", 3), ("upsample_latent1", 2), ("upsample0", 1),
                        ("upsample1", 1), ("upsample2", 1)):
@@ -208,9 +221,11 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code) 
 
 # ---------------------------------------------------------------------- engine
 class _ViTBuffers:
-    def __init__(self, rows: int, dt, dev, out_dt=None):
+    def __init__(self, rows: int, dt, dev, out_dt=None, ln_fold: bool = False):
         self.rows = rows
         self.x = torch.empty(rows, D, dtype=torch.float32, device=dev)
+        # folded LayerNorm: (mean, M2) of each 128-column chunk of the rows in `h` (un-normalised)
+        self.part = torch.empty(rows, D // 128, 2, dtype=torch.float32, device=dev) if ln_fold else None
         self.h = torch.empty(rows, D, dtype=dt, device=dev)
         self.qkv = torch.empty(rows, 3 * D, dtype=dt, device=dev)
         self.a = torch.empty(rows, D, dtype=dt, device=dev)
@@ -334,7 +349,10 @@ class Engine:
         S = IMG_SIZE
         self.x0 = e(3, S, S, dtype=torch.float32)           # network input (normalized, 1536^2)
         self.cols = e(NWIN * PTOK, 768, dtype=vdt)
-        self.vp = _ViTBuffers(NWIN * TOK, vdt, dev, dt)     # patch encoder (35 windows)
+        # patch encoder LayerNorms folded into its GEMMs (pack_weights, _vit); DP_LN_FOLD=0: standalone
+        self.ln_fold = os.environ.get("DP_LN_FOLD", "1") == "1" and \
+            "encoder.patch_encoder.blocks.0.attn.qkv.fold.w" in packed
+        self.vp = _ViTBuffers(NWIN * TOK, vdt, dev, dt, ln_fold=self.ln_fold)     # patch encoder (35 windows)
         # image + FOV encoders, run as one grouped ViT (rows 0..576 image, 577..1153 FOV)
         self.side_vits = ["encoder.image_encoder."] + (["fov.encoder.0."] if self.use_fov else [])
         self.vs = _ViTBuffers(len(self.side_vits) * TOK, vdt, dev, dt)
@@ -440,6 +458,9 @@ class Engine:
             row_off=1)
         for g, pre in enumerate(pres):
             ops.vit_cls_rows(buf.x[g * M:], P[pre + "cls"], P[pre + "pos"], n_img)
+        if G == 1 and buf.part is not None:
+            self._vit_blocks_folded(pres[0], buf, M, hooks)
+            return
         for i in range(DEPTH):
             b = f"blocks.{i}."
             if ln_on:
@@ -460,6 +481,34 @@ class Engine:
             if hooks and i in hooks:
                 hooks[i]()
         norm("norm", buf.out)
+
+    def _vit_blocks_folded(self, pre: str, buf: _ViTBuffers, M: int, hooks=None):
+        """The 24 Blocks with norm1 / norm2 folded across the GEMM boundary (dp_gemm_args.ln_*):
+        `h` carries the un-normalised residual rows in 16 bits and `part` their 128-column chunk
+        statistics, written by the producer (block 0: dp_layernorm_stats; then every proj / fc2
+        epilogue beside its fp32 residual update); qkv / fc1 run on the folded weights
+        (ops.fold_layernorm) and apply LN's per-row mean / rstd in their epilogue.  Same
+        arithmetic as LN -> Linear up to where the 16-bit rounding falls (x instead of LN(x);
+        tools/ln_fold_emul.py: rel-L1 vs fp32 unchanged, 2.377e-3 vs 2.379e-3 bf16)."""
+        P = self.P
+        n_img = M // TOK
+        ops.layernorm_stats(buf.x, buf.h, buf.part, M, D)
+        for i in range(DEPTH):
+            b = f"{pre}blocks.{i}."
+            ops.gemm(buf.h, P[b + "attn.qkv.fold.w"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.fold.b"],
+                     ln_in=(buf.part, P[b + "attn.qkv.fold.s"]))
+            if "attn" not in _ABLATE:
+                ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
+            ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
+                     gamma=P[b + "ls1.gamma"], accumulate=True, ln_out=(buf.h, buf.part))
+            ops.gemm(buf.h, P[b + "mlp.fc1.fold.w"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.fold.b"],
+                     act=DP_ACT_GELU, ln_in=(buf.part, P[b + "mlp.fc1.fold.s"]))
+            last = i == DEPTH - 1    # the final norm reads x itself
+            ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
+                     gamma=P[b + "ls2.gamma"], accumulate=True, ln_out=None if last else (buf.h, buf.part))
+            if hooks and i in hooks:
+                hooks[i]()
+        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,

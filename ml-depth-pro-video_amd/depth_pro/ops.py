@@ -142,12 +142,17 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          head_corr: Optional[torch.Tensor] = None,
          A_off: int = 0, C_off: int = 0, B_off: int = 0, tile: int = 0,
          workspace: Optional[torch.Tensor] = None,
-         plan_only: bool = False, border_corr: Optional[torch.Tensor] = None):
+         plan_only: bool = False, border_corr: Optional[torch.Tensor] = None,
+         ln_out: Optional[tuple] = None, ln_in: Optional[tuple] = None, ln_eps: float = 1e-6):
     """dp_gemm. `A_off`/`B_off`/`C_off` are element offsets into A / B / C (sub-views, e.g. a
     K slice of a split-K GEMM: A_off = B_off = k0 with lda / ldb the full row lengths).
 
     `workspace` (or the one set by `use_workspace`) enables the stream-K engine.
     `plan_only=True` launches nothing and returns (tile, workgroups) from dp_gemm_plan.
+    Folded LayerNorm (dp_gemm_args.ln_*): `ln_out=(xb, part)` -- the residual GEMM also writes the
+    new C rows in 16 bits to `xb` and their 128-column chunk statistics to `part`; `ln_in=(part,
+    colsum)` -- A holds un-normalised 16-bit rows with statistics `part`, B / bias are folded
+    (`fold_layernorm`) and `colsum` = the row sums of B.
     """
     a = _gemm_args(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc, conv=conv, relu_a=relu_a, bias=bias,
                    act=act, gamma=gamma, pos=pos, ldpos=ldpos, pos_group=pos_group, pos_off=pos_off, R1=R1,
@@ -155,6 +160,17 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
                    row_group_out=row_group_out, row_off=row_off, head_w=head_w, head_b=head_b,
                    head_corr=head_corr, A_off=A_off, C_off=C_off, B_off=B_off, tile=tile, workspace=workspace,
                    border_corr=border_corr)
+    if ln_out is not None:
+        xb, part = ln_out
+        if xb.numel() < (M - 1) * a.ldc + N or part.numel() < M * (N // 128) * 2 or part.dtype != torch.float32 \
+                or xb.dtype != B.dtype:
+            raise _lib.DPError("dp_gemm: ln_out buffers too small or of the wrong type")
+        a.ln_xb_out, a.ln_part_out = xb.data_ptr(), part.data_ptr()
+    if ln_in is not None:
+        part, colsum = ln_in
+        if part.numel() < M * (K // 128) * 2 or colsum.numel() < N or colsum.dtype != torch.float32:
+            raise _lib.DPError("dp_gemm: ln_in buffers too small or of the wrong type")
+        a.ln_part_in, a.ln_colsum, a.ln_eps = part.data_ptr(), colsum.data_ptr(), float(ln_eps)
     if plan_only:
         t, g = ctypes.c_int32(), ctypes.c_int32()
         check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
@@ -267,6 +283,31 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor
     with _Timed("layernorm", 0.0, (rows, cols), y.dtype):
         check(_lib.load().dp_layernorm(x.data_ptr(), cols, w.data_ptr(), b.data_ptr(), y.data_ptr(), cols,
                                        rows, cols, eps, dtype_code(y.dtype), _stream(y)), "dp_layernorm")
+
+
+def layernorm_stats(x: torch.Tensor, xb: torch.Tensor, part: torch.Tensor, rows: int, cols: int) -> None:
+    """dp_layernorm_stats: x (fp32 rows) -> xb (16 bits) + 128-column chunk statistics `part` --
+    the input side of a folded LayerNorm for rows no residual GEMM produced (ViT block 0)."""
+    if x.numel() < rows * cols or xb.numel() < rows * cols or part.numel() < rows * (cols // 128) * 2:
+        raise _lib.DPError("dp_layernorm_stats: buffers smaller than rows * cols")
+    with _Timed("layernorm", 0.0, (rows, cols), xb.dtype):
+        check(_lib.load().dp_layernorm_stats(x.data_ptr(), cols, rows, cols, xb.data_ptr(), cols, part.data_ptr(),
+                                             dtype_code(xb.dtype), _stream(xb)), "dp_layernorm_stats")
+
+
+def fold_layernorm(w: torch.Tensor, b: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, dt: torch.dtype,
+                   col_scale: Optional[torch.Tensor] = None):
+    """The consumer side of a LayerNorm folded into the Linear after it (pack time):
+    LN(x) W^T + b = rstd * (x (W o ln_w)^T - mean * S) + (b + W ln_b), so the GEMM takes the
+    un-normalised rows with B = W o ln_w (per input column; times `col_scale` per output, e.g.
+    the qkv's log2q gamma), bias = (b + W ln_b) * col_scale and S = the row sums of B exactly as
+    the 16-bit values the MFMA multiplies (fp64 sums, fp32 result).  Returns (B, bias, S)."""
+    w64, b64 = w.double(), b.double()
+    s = torch.ones(w.shape[0], dtype=torch.float64, device=w.device) if col_scale is None else col_scale.double()
+    wf = (w64 * ln_w.double()[None, :] * s[:, None]).to(dt).contiguous()
+    bias = ((b64 + w64 @ ln_b.double()) * s).float().contiguous()
+    colsum = wf.double().sum(1).float().contiguous()
+    return wf, bias, colsum
 
 
 def layernorm_grouped(x: torch.Tensor, ws, bs, y: torch.Tensor, rows_per_group: int, cols: int,

@@ -882,3 +882,92 @@ def test_patch_conv3x3_head_epilogues(cuda, dt):
     r = F.conv_transpose2d(h0, wd, bd, stride=2)
     r = F.relu(F.conv2d(F.relu(F.conv2d(r, w2, b2, padding=1)), w4.reshape(1, 32, 1, 1), torch.tensor([0.25])))
     close(d1, r[0, 0], dt, "cv3 head HEAD_PS")
+
+
+def _chunk_stats(x):
+    """(mean, M2) of each 128-column chunk of fp32 rows x, in fp64 (the folded-LN statistics)."""
+    c = x.double().reshape(x.shape[0], -1, 128)
+    mu = c.mean(-1)
+    return torch.stack((mu, ((c - mu[..., None]) ** 2).sum(-1)), -1)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_layernorm_stats(cuda, dt):
+    """dp_layernorm_stats: x in 16 bits (exactly x.to(dt)) + per-128-column (mean, M2)."""
+    g = torch.Generator().manual_seed(11)
+    rows = 1155
+    x = torch.randn(rows, 1024, generator=g) * 3 + torch.randn(rows, 1, generator=g) * 2
+    xb = torch.empty(rows, 1024, dtype=dt, device=cuda)
+    part = torch.empty(rows, 8, 2, device=cuda)
+    ops.layernorm_stats(x.to(cuda), xb, part, rows, 1024)
+    assert torch.equal(xb.cpu(), x.to(dt))
+    ref = _chunk_stats(x)
+    np.testing.assert_allclose(part.cpu().double().numpy(), ref.numpy(), rtol=2e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,K", [(20195, 1024), (577, 4096)])
+def test_gemm_8ph320_ln_producer(cuda, dt, M, K):
+    """Folded-LN producer (the ViT proj / fc2 with ln_out): C is bit-identical to the plain
+    residual launch, xb == the new C rows in 16 bits, part == their 128-column chunk stats."""
+    g = torch.Generator().manual_seed(M + K)
+    N = 1024
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    gamma = (0.1 + 0.02 * torch.randn(N, generator=g)).to(cuda)
+    C0 = (torch.randn(M, N, generator=g) * 2 + 0.5).to(cuda)
+    C1, C2 = C0.clone(), C0.clone()
+    xb = torch.empty(M, N, dtype=dt, device=cuda)
+    part = torch.empty(M, N // 128, 2, device=cuda)
+    from depth_pro._lib import DP_TILE_8PH_320x256
+
+    kw = dict(M=M, N=N, K=K, bias=bias, gamma=gamma, accumulate=True)
+    ops.gemm(A, B, C1, tile=DP_TILE_8PH_320x256, **kw)
+    ops.gemm(A, B, C2, ln_out=(xb, part), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C2)
+    assert torch.equal(xb, C2.to(dt))
+    np.testing.assert_allclose(part.cpu().double().numpy(), _chunk_stats(C2.cpu()).numpy(), rtol=5e-5, atol=2e-4)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("act,col_scale", [(0, True), (DP_ACT_GELU, False)])
+def test_gemm_8ph320_ln_consumer(cuda, dt, act, col_scale):
+    """Folded-LN consumer (the ViT qkv / fc1 with ln_in): GEMM over the un-normalised 16-bit rows
+    with ops.fold_layernorm's weights == LN(x) W^T + b (then * the per-column scale, or GELU) in
+    fp32; its error vs that reference is no larger than the unfolded LN -> 16-bit -> GEMM path's."""
+    g = torch.Generator().manual_seed(5 + act)
+    M, K, N = 20195, 1024, 3072 if col_scale else 4096
+    x = torch.randn(M, K, generator=g) * 2 + torch.randn(M, 1, generator=g)
+    x[:, 7] += 40.0                                          # an outlier channel, as DINOv2's
+    w = torch.randn(N, K, generator=g) * K ** -0.5
+    b = torch.randn(N, generator=g) * 0.02
+    lw = 1.0 + 0.1 * torch.randn(K, generator=g)
+    lb = 0.02 * torch.randn(K, generator=g)
+    cs = ops.log2q_gamma(16, 64, "cpu") if col_scale else None
+    xd = x.to(cuda)
+    xb = torch.empty(M, K, dtype=dt, device=cuda)
+    part = torch.empty(M, K // 128, 2, device=cuda)
+    ops.layernorm_stats(xd, xb, part, M, K)
+    wf, bf, sf = ops.fold_layernorm(w.to(cuda), b.to(cuda), lw.to(cuda), lb.to(cuda), dt,
+                                    None if cs is None else cs.to(cuda))
+    out = torch.empty(M, N, dtype=dt, device=cuda)
+    ops.gemm(xb, wf, out, M=M, N=N, K=K, bias=bf, act=act, ln_in=(part, sf))
+    # unfolded: LN kernel -> 16-bit -> GEMM with bias (and gamma)
+    h = torch.empty(M, K, dtype=dt, device=cuda)
+    ops.layernorm(xd, lw.to(cuda), lb.to(cuda), h, M, K)
+    out2 = torch.empty(M, N, dtype=dt, device=cuda)
+    ops.gemm(h, w.to(dt).to(cuda), out2, M=M, N=N, K=K, bias=b.to(cuda), act=act,
+             gamma=None if cs is None else cs.to(cuda))
+    torch.cuda.synchronize()
+    ref = F.linear(F.layer_norm(x, (K,), lw, lb, 1e-6), w, b)
+    if act == DP_ACT_GELU:
+        ref = F.gelu(ref)
+    if cs is not None:
+        ref = ref * cs
+    e1 = ((out.float().cpu() - ref).abs().mean() / ref.abs().mean()).item()
+    e2 = ((out2.float().cpu() - ref).abs().mean() / ref.abs().mean()).item()
+    print(f"\nLN fold {dt} act={act}: folded rel-L1 {e1:.3e}, unfolded {e2:.3e}")
+    assert e1 < (8e-3 if dt == torch.bfloat16 else 1.5e-3)
+    assert e1 < 1.25 * e2 + 1e-5

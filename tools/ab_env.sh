@@ -1,0 +1,24 @@
+#!/bin/bash
+# In-frame A/B of environment settings (product switches such as DP_LN_FOLD=0), alternating,
+# 2 rounds, bench.py lines into gpurun_out/<tag>/ (run on the gpurun box from the repo root).
+# Usage: tools/ab_env.sh <tag> "VAR=a" "VAR=b" ...
+set -eo pipefail
+TAG=$1; shift
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+for R in 1 2; do
+  i=0
+  for E in "$@"; do
+    i=$((i + 1))
+    env $E timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $OUT/ab_${i}_$R.json 2> $OUT/ab_${i}_$R.err
+  done
+done
+python - "$OUT" "$@" <<'PY'
+import json, sys, glob
+out, envs = sys.argv[1], sys.argv[2:]
+for i, e in enumerate(envs, 1):
+    for f in sorted(glob.glob(f"{out}/ab_{i}_*.json")):
+        d = json.loads(open(f).read().strip().splitlines()[-1])
+        dk = d["roofline"]["dominant_kernel"]
+        print(e, f.split("/")[-1], d["value"], d["ms_per_step"], d["parity"]["depth_rel_l1"], dk["kind"], dk["avg_us"])
+PY
