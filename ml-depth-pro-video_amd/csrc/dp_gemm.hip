@@ -248,7 +248,12 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // (load-free with a 16-bit C, or the fp32 residual accumulate without activation) -- the
   // planner's dense 320 x 256 launches (ViT qkv / proj / fc2) run on it (qkv 130.6 -> 115.8,
   // fc2 149.6 -> 142.0 us, profiles/r03d_8ph320; debug 1 << 15: off)
-  if (lnp || lnc) tile = DP_TILE_8PH_320x256;   // the engine with the folded-LN epilogues
+  // the engines with the folded-LN epilogues: the 8-phase 320 x 256 one (producer and consumer),
+  // and for a consumer the planner put on the persistent 8-phase engine (the ViT fc1) that one,
+  // given a workspace for its merged row statistics (debug 1 << 25: the 320 x 256 engine)
+  const bool lnc_p8 = lnc && tile == DP_TILE_P8PH_256x256 && ws_ok && !(dbg & (1 << 25)) &&
+                      (long long)(a->M + 255) / 256 * 256 * 8 <= (long long)SK_TILE_F * 4;
+  if ((lnp || lnc) && !lnc_p8) tile = DP_TILE_8PH_320x256;
   if (tile == DP_TILE_8PH_320x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_BIG_320x256 && !(dbg & (1 << 15)))) {
     const bool plain = a->a_mode == DP_A_DENSE && !a->relu_a && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
                        !a->R1 && !a->R2 && !a->pos && !a->row_group && !a->head_w && !a->head_corr &&
@@ -288,6 +293,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.head_w = a->head_w; p.head_b = a->head_b; p.head_corr = a->head_corr;
   p.ln_part_out = a->ln_part_out; p.ln_xb_out = (u16*)a->ln_xb_out;
   p.ln_part_in = a->ln_part_in; p.ln_colsum = a->ln_colsum; p.ln_eps = a->ln_eps;
+  p.ln_rs = nullptr;
   p.tiles_n = 1;
   p.tiles_m = 1;
   if (tile == DP_TILE_STREAMK_256x256) {
@@ -337,6 +343,15 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool conv = a->a_mode == DP_A_CONV;
   if (tile == DP_TILE_STREAMK_256x256) return launch_part_sk(p, conv, a->workspace, a->dtype == DP_BF16, s);
+  if (tile == DP_TILE_P8PH_256x256 && a->ln_part_in) {
+    // folded-LN consumer on the persistent engine: merge each row's chunk statistics into
+    // (rstd, -rstd * mean) in the workspace's first partial-tile slot (no stream-K launch uses
+    // it meanwhile: the workspace belongs to this stream), read by the epilogue via LDS
+    float* rs = (float*)((char*)a->workspace + SK_FLAG_BYTES);
+    hipLaunchKernelGGL(ln_merge_kernel, dim3((a->M + 255) / 256), dim3(256), 0, s, a->ln_part_in, a->M, a->ln_eps, rs);
+    DP_CHECK_LAUNCH();
+    p.ln_rs = rs;
+  }
   return launch_tile(p, tile, conv, a->dtype == DP_BF16, s);
 }
 

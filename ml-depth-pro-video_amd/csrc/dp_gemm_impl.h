@@ -76,6 +76,8 @@ struct GemmP {
   const float* ln_part_in; // consumer: the A rows' chunk statistics ([M][K/128][2])
   const float* ln_colsum;  // consumer: sum_k B[n][k]
   float ln_eps;
+  const float* ln_rs;      // consumer on the persistent 8-phase engine: per row (rstd, -rstd * mean),
+                           // merged from ln_part_in by ln_merge_kernel into the GEMM workspace
   // dp_gemm_grouped: `groups` problems of one shape in one launch (workgroup range g * tiles_m *
   // tiles_n ... covers problem g, whose operand pointers are grp[g]); 1 otherwise
   int groups;
@@ -1812,17 +1814,17 @@ int launch_8ph(const GemmP& p0, bool conv, hipStream_t s) {
 // (filled by LDS-DMA with the tile's loads), so the epilogue issues no global load: hipcc
 // would put a vmcnt(0) in front of one -- a wait for every LDS-DMA in flight, i.e. the next
 // tile's first K steps.
-template <typename K_, int ACT, bool HG, bool DCV>
+template <typename K_, int ACT, bool HG, bool DCV, bool LNC = false>
 __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)[8][4], char* slab,
                                                   const float* cst, int lane, int m_base, int n_base,
-                                                  __amdgpu_buffer_rsrc_t crs) {
+                                                  __amdgpu_buffer_rsrc_t crs, const char* rstat = nullptr) {
   constexpr int FM = 8, FN = 4, TN = 64, PF = 1, CH = TN / 8, RPI = 64 / CH;
   const int t = lane & 15, g = lane >> 4;
   f32x4_t bias[FN], gam[FN];
   #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     bias[fn] = *(const f32x4_t*)(cst + fn * 16 + 4 * g);
-    if constexpr (HG) gam[fn] = *(const f32x4_t*)(cst + 64 + fn * 16 + 4 * g);
+    if constexpr (HG || LNC) gam[fn] = *(const f32x4_t*)(cst + 64 + fn * 16 + 4 * g);   // LNC: colsum
   }
   #pragma unroll
   for (int f0 = 0; f0 < FM; f0 += PF) {
@@ -1832,7 +1834,17 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
       for (int fn = 0; fn < FN; ++fn) {
         // packed-f32 arithmetic (the 4 columns of a lane as one vector): same values as the
         // scalar epilogue_mfma, half the VALU issue slots
-        f32x4_t x = acc[f0 + fm][fn] + bias[fn];
+        f32x4_t x;
+        if constexpr (LNC) {
+          // folded LayerNorm: row r of the wave group's 128 lives in the const slot of its wave
+          // wn' = r / 32 (each wave DMAs 32 rows' (rstd, -rstd * mean), issue_cst)
+          const int r = (f0 + fm) * 16 + t;
+          const float2 st = *(const float2*)(rstat + (r >> 5) * 2048 + (r & 31) * 8);
+          x = __builtin_elementwise_fma(acc[f0 + fm][fn], (f32x4_t)(st.x),
+                                        __builtin_elementwise_fma(gam[fn], (f32x4_t)(st.y), bias[fn]));
+        } else {
+          x = acc[f0 + fm][fn] + bias[fn];
+        }
         if constexpr (ACT == DP_ACT_RELU) {
           #pragma unroll
           for (int r = 0; r < 4; ++r) x[r] = fmaxf(x[r], 0.f);
@@ -1872,7 +1884,7 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
   }
 }
 
-template <typename K_, bool RELU, int ACT, bool HG, bool DCV = false>
+template <typename K_, bool RELU, int ACT, bool HG, bool DCV = false, bool LNC = false>
 __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   constexpr int HALF = 128 * 128;   // bytes: 128 rows x 64 16-bit
   constexpr int TILEB = 4 * HALF;   // A0 A1 B0 B1
@@ -2001,13 +2013,19 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   // column constants of tile t -> this wave's const slot `par`: ONE LDS-DMA piece per wave
   // (lanes 0-15: bias of the wave's 64 columns, 16-31: gamma, 32-63 repeat 0-31), issued
   // with the tile's loads and retired by the same counted waits (only this wave reads it)
+  // LNC (folded-LayerNorm consumer): lanes 16-31 bring the column sums instead of gamma and
+  // lanes 32-47 the (rstd, -rstd * mean) of 32 of the wave group's 128 rows (2 rows per lane,
+  // rows wn * 32 ..), so the 4 waves of a group hold its rows between them (read across waves
+  // in the epilogue: that tile's whole K loop, with its barriers, lies between)
   auto issue_cst = [&](int t, int par) {
     int tm, tn;
     tile_coords(p, t, tm, tn);
     const int l = lane & 15, n = tn * 256 + wn * TN + 4 * l;
     const float* src;
-    if ((lane & 16) == 0) src = p.bias ? p.bias + n : (const float*)g_zero_page + 4 * l;
-    else src = HG ? p.gamma + n : (const float*)g_zero_page + 4 * l;
+    if ((lane & 16) == 0 && lane < 32) src = p.bias ? p.bias + n : (const float*)g_zero_page + 4 * l;
+    else if (lane < 32) src = HG ? p.gamma + n : LNC ? p.ln_colsum + n : (const float*)g_zero_page + 4 * l;
+    else if (LNC && lane < 48) src = p.ln_rs + 2 * (tm * 256 + wm * TM + wn * 32 + 2 * (lane - 32));
+    else src = (const float*)g_zero_page + 4 * l;
     glds16(src, __builtin_amdgcn_readfirstlane(lds_addr(smem)) + RING + 8 * SLAB + (wave_u * 2 + par) * CST);
   };
 
@@ -2066,12 +2084,36 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     int tm, tn;
     tile_coords(p, t_cur, tm, tn);
     const float* cst = (const float*)(smem + RING + 8 * SLAB + (wave * 2 + (i & 1)) * CST);
-    epilogue_mfma_buf<K_, ACT, HG, DCV>(p, acc, slab, cst, lane, tm * 256 + wm * TM, tn * 256 + wn * TN, crs);
+    const char* rstat = smem + RING + 8 * SLAB + (wm * 8 + (i & 1)) * CST + 512;   // wave group's row stats
+    epilogue_mfma_buf<K_, ACT, HG, DCV, LNC>(p, acc, slab, cst, lane, tm * 256 + wm * TM, tn * 256 + wn * TN, crs,
+                                             rstat);
     if (t_nxt < 0) break;
     t_cur = t_nxt;
     t_nxt = next_tile(t_cur);
   }
   if (wm == 0) bar();
+}
+
+// Folded LayerNorm, consumer on the persistent 8-phase engine: per row (rstd, -rstd * mean) from
+// its 8 chunk statistics (K = 1024; Chan's merge, as epilogue_mfma_lnc), one thread per row.
+__global__ void __launch_bounds__(256) ln_merge_kernel(const float* __restrict__ part, int M, float eps,
+                                                       float* __restrict__ out) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const f32x4_t* pp = (const f32x4_t*)(part + (long long)m * 16);
+  f32x4_t c[4];
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = pp[i];
+  const float mean = (((c[0][0] + c[0][2]) + (c[1][0] + c[1][2])) + ((c[2][0] + c[2][2]) + (c[3][0] + c[3][2]))) *
+                     (1.f / 8);
+  float m2 = 0.f;
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float d0 = c[i][0] - mean, d1 = c[i][2] - mean;
+    m2 += (c[i][1] + 128.f * d0 * d0) + (c[i][3] + 128.f * d1 * d1);
+  }
+  const float rs = rsqrtf(m2 * (1.f / 1024) + eps);
+  *(float2*)(out + 2LL * m) = make_float2(rs, -rs * mean);
 }
 
 template <typename K_>
@@ -2095,6 +2137,14 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
     return 0;
   }
   if (p.store_mode != DP_STORE_ROWS) return DP_ERR_ARG;
+  if (p.ln_rs) {   // folded-LayerNorm consumer (the ViT fc1): dense, no ReLU prologue, no gamma
+    if (p.relu_a || p.gamma) return DP_ERR_ARG;
+    if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, false, DP_ACT_NONE, false, false, true>), grid, dim3(512), 0, s, p);
+    else if (ea == DP_ACT_GELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, false, DP_ACT_GELU, false, false, true>), grid, dim3(512), 0, s, p);
+    else return DP_ERR_ARG;
+    DP_CHECK_LAUNCH();
+    return 0;
+  }
 #define DP_P8(R_, G_) do { \
     if (ea == DP_ACT_NONE) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_NONE, G_>), grid, dim3(512), 0, s, p); \
     else if (ea == DP_ACT_RELU) hipLaunchKernelGGL((gemm_p8ph_kernel<K_, R_, DP_ACT_RELU, G_>), grid, dim3(512), 0, s, p); \

@@ -932,8 +932,9 @@ def test_gemm_8ph320_ln_producer(cuda, dt, M, K):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("act,col_scale", [(0, True), (DP_ACT_GELU, False)])
-def test_gemm_8ph320_ln_consumer(cuda, dt, act, col_scale):
+@pytest.mark.parametrize("act,col_scale,engine", [(0, True, "8ph320"), (DP_ACT_GELU, False, "8ph320"),
+                                                  (DP_ACT_GELU, False, "p8ph")])
+def test_gemm_8ph320_ln_consumer(cuda, dt, act, col_scale, engine):
     """Folded-LN consumer (the ViT qkv / fc1 with ln_in): GEMM over the un-normalised 16-bit rows
     with ops.fold_layernorm's weights == LN(x) W^T + b (then * the per-column scale, or GELU) in
     fp32; its error vs that reference is no larger than the unfolded LN -> 16-bit -> GEMM path's."""
@@ -952,8 +953,14 @@ def test_gemm_8ph320_ln_consumer(cuda, dt, act, col_scale):
     ops.layernorm_stats(xd, xb, part, M, K)
     wf, bf, sf = ops.fold_layernorm(w.to(cuda), b.to(cuda), lw.to(cuda), lb.to(cuda), dt,
                                     None if cs is None else cs.to(cuda))
+    from depth_pro._lib import DP_TILE_8PH_320x256, DP_TILE_P8PH_256x256
+
     out = torch.empty(M, N, dtype=dt, device=cuda)
-    ops.gemm(xb, wf, out, M=M, N=N, K=K, bias=bf, act=act, ln_in=(part, sf))
+    ws = ops.gemm_workspace(cuda) if engine == "p8ph" else None
+    kw = dict(M=M, N=N, K=K, bias=bf, act=act, ln_in=(part, sf), workspace=ws)
+    tile, _ = ops.gemm(xb, wf, out, plan_only=True, **kw)
+    assert tile == (DP_TILE_P8PH_256x256 if engine == "p8ph" else DP_TILE_8PH_320x256)
+    ops.gemm(xb, wf, out, **kw)
     # unfolded: LN kernel -> 16-bit -> GEMM with bias (and gamma)
     h = torch.empty(M, K, dtype=dt, device=cuda)
     ops.layernorm(xd, lw.to(cuda), lb.to(cuda), h, M, K)
@@ -968,6 +975,6 @@ def test_gemm_8ph320_ln_consumer(cuda, dt, act, col_scale):
         ref = ref * cs
     e1 = ((out.float().cpu() - ref).abs().mean() / ref.abs().mean()).item()
     e2 = ((out2.float().cpu() - ref).abs().mean() / ref.abs().mean()).item()
-    print(f"\nLN fold {dt} act={act}: folded rel-L1 {e1:.3e}, unfolded {e2:.3e}")
+    print(f"\nLN fold {dt} act={act} {engine}: folded rel-L1 {e1:.3e}, unfolded {e2:.3e}")
     assert e1 < (8e-3 if dt == torch.bfloat16 else 1.5e-3)
     assert e1 < 1.25 * e2 + 1e-5

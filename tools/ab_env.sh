@@ -10,7 +10,8 @@ for R in 1 2; do
   i=0
   for E in "$@"; do
     i=$((i + 1))
-    env $E timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 40 > $OUT/ab_${i}_$R.json 2> $OUT/ab_${i}_$R.err
+    AB=""; case "$E" in *DP_GEMM_DEBUG*|*DP_ABLATE*) AB="--ab" ;; esac
+    env $E timeout -k 10 300 python -u bench.py $AB --no-cpu-baseline --steps 40 > $OUT/ab_${i}_$R.json 2> $OUT/ab_${i}_$R.err
   done
 done
 python - "$OUT" "$@" <<'PY'
@@ -20,5 +21,6 @@ for i, e in enumerate(envs, 1):
     for f in sorted(glob.glob(f"{out}/ab_{i}_*.json")):
         d = json.loads(open(f).read().strip().splitlines()[-1])
         dk = d["roofline"]["dominant_kernel"]
-        print(e, f.split("/")[-1], d["value"], d["ms_per_step"], d["parity"]["depth_rel_l1"], dk["kind"], dk["avg_us"])
+        v = d["value"] if d.get("value") is not None else d.get("ab_fps")
+        print(e, f.split("/")[-1], v, d["ms_per_step"], d["parity"]["depth_rel_l1"], dk["kind"], dk["avg_us"])
 PY
