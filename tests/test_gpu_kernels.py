@@ -376,8 +376,10 @@ def test_resize_and_infer_epilogue_bicubic(cuda, HW):
     inv = canon * (W / f_ref)
     if (H, W) != (1536, 1536):
         inv = F.interpolate(inv, size=(H, W), mode="bicubic", align_corners=False)
-    dref = 1.0 / torch.clamp(inv, 1e-4, 1e4)
-    np.testing.assert_allclose(depth.cpu().numpy(), dref[0, 0].numpy(), rtol=5e-5, atol=1e-6)
+    # compared as inverse depth (1 / depth = the clamped resize): bicubic overshoot on this noise
+    # puts some pixels near the 1e-4 clamp, where depth itself magnifies ulp-level differences
+    np.testing.assert_allclose(1.0 / depth.cpu().numpy(), torch.clamp(inv, 1e-4, 1e4)[0, 0].numpy(),
+                               rtol=2e-5, atol=2e-6)
     with pytest.raises(ValueError):
         ops.resize(x.to(cuda), out, "nearest")
 

@@ -236,10 +236,15 @@ def test_infer_bicubic_matches_torch_resizes(model):
     two resizes, depth_pro.py:268-298)."""
     import torch.nn.functional as F
 
+    from depth_pro import ops
+
     m, transform = model
     x = transform(frame(3, 720, 1280))
     p = m.infer(x, interpolation_mode="bicubic")
-    xr = F.interpolate(x[None].float(), size=(1536, 1536), mode="bicubic", align_corners=False)
+    # the network input through dp_resize's bicubic (its parity with torch: the kernel test), so the
+    # forward sees identical bits; the epilogue's bicubic resize back is checked against torch here
+    xr = torch.empty(1, 3, 1536, 1536, device=x.device)
+    ops.resize(x, xr[0], "bicubic")
     c, fov = m.forward(xr)
     f_px = 0.5 * 1280 / torch.tan(0.5 * torch.deg2rad(fov.float()))
     inv = F.interpolate(c * (1280 / f_px), size=(720, 1280), mode="bicubic", align_corners=False)
