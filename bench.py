@@ -185,6 +185,10 @@ def launch_ranks(n: int) -> None:
     sys.exit(subprocess.call(cmd))
 
 
+# environment switches and their product defaults: a bench line is only printed for the defaults
+AB_KNOBS = {"DP_ABLATE": "0", "DP_GEMM_DEBUG": "0", "DP_ATTN_DEBUG": "0", "DP_SIDE_GATE": "0", "DP_LN_FOLD": "1"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,15 +201,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pool", type=int, default=4, help="distinct resident frames per rank")
     ap.add_argument("--ab", action="store_true",
-                    help="A/B timing run (tools/ab_bench.sh): allows DP_GEMM_DEBUG / DP_ABLATE and reports "
+                    help="A/B timing run (tools/ab_env.sh): allows the AB_KNOBS switches off their defaults and reports "
                          "'ab_fps' instead of a bench 'value'")
     args = ap.parse_args()
 
     # a run whose results are wrong by construction (ablations) or whose schedule is not the product's
     # (debug switches) prints no value
-    forced = [v for v in ("DP_ABLATE", "DP_GEMM_DEBUG", "DP_ATTN_DEBUG") if os.environ.get(v, "") not in ("", "0")]
+    forced = [v for v, dflt in AB_KNOBS.items() if os.environ.get(v, dflt) not in ("", dflt)]
     if forced and not args.ab:
-        refuse(f"{', '.join(forced)} set: ablation / debug switches make the frame invalid (use --ab)", 3)
+        refuse(f"{', '.join(forced)} set: ablation / debug / schedule switches off their defaults make the "
+               f"frame invalid or not the product's (use --ab)", 3)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -412,7 +417,7 @@ def main():
         if args.ab:        # A/B timing run: not a bench result
             out["metric"] = "A/B timing run (DP_GEMM_DEBUG / DP_ABLATE allowed): not a bench result"
             out["ab_fps"], out["value"] = out["value"], None
-            out["ab_env"] = {v: os.environ.get(v, "") for v in ("DP_ABLATE", "DP_GEMM_DEBUG", "DP_ATTN_DEBUG")}
+            out["ab_env"] = {v: os.environ.get(v, "") for v in AB_KNOBS}
         elif world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out), flush=True)

@@ -1826,6 +1826,16 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
     bias[fn] = *(const f32x4_t*)(cst + fn * 16 + 4 * g);
     if constexpr (HG || LNC) gam[fn] = *(const f32x4_t*)(cst + 64 + fn * 16 + 4 * g);   // LNC: colsum
   }
+  // folded LayerNorm: row r = fm * 16 + t of the wave group's 128 lives in the const slot of its
+  // wave wn' = r / 32 (each wave DMAs 32 rows' (rstd, -rstd * mean), issue_cst); all 8 read up front
+  float2 rst[LNC ? FM : 1];
+  if constexpr (LNC) {
+    #pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int r = fm * 16 + t;
+      rst[fm] = *(const float2*)(rstat + (r >> 5) * 2048 + (r & 31) * 8);
+    }
+  }
   #pragma unroll
   for (int f0 = 0; f0 < FM; f0 += PF) {
     #pragma unroll
@@ -1836,12 +1846,8 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
         // scalar epilogue_mfma, half the VALU issue slots
         f32x4_t x;
         if constexpr (LNC) {
-          // folded LayerNorm: row r of the wave group's 128 lives in the const slot of its wave
-          // wn' = r / 32 (each wave DMAs 32 rows' (rstd, -rstd * mean), issue_cst)
-          const int r = (f0 + fm) * 16 + t;
-          const float2 st = *(const float2*)(rstat + (r >> 5) * 2048 + (r & 31) * 8);
-          x = __builtin_elementwise_fma(acc[f0 + fm][fn], (f32x4_t)(st.x),
-                                        __builtin_elementwise_fma(gam[fn], (f32x4_t)(st.y), bias[fn]));
+          x = __builtin_elementwise_fma(acc[f0 + fm][fn], (f32x4_t)(rst[f0 + fm].x),
+                                        __builtin_elementwise_fma(gam[fn], (f32x4_t)(rst[f0 + fm].y), bias[fn]));
         } else {
           x = acc[f0 + fm][fn] + bias[fn];
         }

@@ -413,6 +413,10 @@ class Engine:
         # takes one exp2 per score (dp_attention_log2q)
         self.qkv_gamma = ops.log2q_gamma(HEADS, D // HEADS, dev)
         self.serial_side = False   # True: every launch on the current stream, in one order (profiling)
+        # side encoders gated block by block into chosen patch-encoder launches (_forward):
+        # DP_SIDE_GATE="release:join" points, e.g. "qkv:proj" or "fc2:fc1"; unset: free-running
+        g = os.environ.get("DP_SIDE_GATE", "")
+        self.side_gate = tuple(g.split(":")) if ":" in g else None
         # device status of the current frame: [error word of each workspace (forward's end),
         # non-finite output count (the infer epilogue)]
         self._wss = [self.ws_main, self.ws_dec]
@@ -424,9 +428,17 @@ class Engine:
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
 
     # ------------------------------------------------------------------ ViT
-    def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
+    def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, sync=None):
         """timm forward_features (vit_factory.py:97-99 -> vision_transformer.py): patch embed + cls /
         pos, 24 Blocks, final norm; `hooks[i]()` runs after block i (encoder.py:133-144).
+        `sync` (optional): sync(point, i) before block i's qkv / proj / fc1 / fc2 ("qkv", "proj",
+        "fc1", "fc2") -- where the side-encoder schedule gates the other stream (Engine._forward)."""
+        for _ in self._vit_steps(pres, buf, n_img, cols_off_rows, hooks, sync):
+            pass
+
+    def _vit_steps(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, sync=None):
+        """`_vit` as a generator: yields after the embedding and after each Block (the final norm
+        runs on the last step) -- lets a caller issue another stream's ViT block by block.
 
         `pres`: the weight prefixes of G ViTs of one shape over the same im2col rows (G = 2: the
         image and FOV encoders, encoder.py:308-311 and fov.py:66-72); ViT g owns rows
@@ -435,6 +447,7 @@ class Engine:
         P, M = self.P, n_img * TOK
         G = len(pres)
         ln_on, gemm_on = "ln" not in _ABLATE, "vitgemm" not in _ABLATE
+        sync = sync or (lambda what, i: None)
 
         def lin(A, key, C, N, K, a_rows=True, **kw):
             """The G problems' `key` Linear: A rows / C rows of problem g at g * M (A shared when
@@ -459,56 +472,73 @@ class Engine:
         for g, pre in enumerate(pres):
             ops.vit_cls_rows(buf.x[g * M:], P[pre + "cls"], P[pre + "pos"], n_img)
         if G == 1 and buf.part is not None:
-            self._vit_blocks_folded(pres[0], buf, M, hooks)
+            yield from self._vit_blocks_folded(pres[0], buf, M, hooks, sync)
             return
+        yield
         for i in range(DEPTH):
             b = f"blocks.{i}."
+            sync("qkv", i)
             if ln_on:
                 norm(b + "norm1", buf.h)
             if gemm_on:
                 lin(buf.h, b + "attn.qkv.weight", buf.qkv, 3 * D, D, bias=b + "attn.qkv.bias", gamma=self.qkv_gamma)
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, G * n_img, TOK, HEADS, D // HEADS, log2q=True)
+            sync("proj", i)
             if gemm_on:
                 lin(buf.a, b + "attn.proj.weight", buf.x, D, D, bias=b + "attn.proj.bias", gamma=b + "ls1.gamma",
                     accumulate=True)
             if ln_on:
                 norm(b + "norm2", buf.h)
+            sync("fc1", i)
             if gemm_on:
                 lin(buf.h, b + "mlp.fc1.weight", buf.m, MLP_DIM, D, bias=b + "mlp.fc1.bias", act=DP_ACT_GELU)
+            sync("fc2", i)
+            if gemm_on:
                 lin(buf.m, b + "mlp.fc2.weight", buf.x, D, MLP_DIM, bias=b + "mlp.fc2.bias", gamma=b + "ls2.gamma",
                     accumulate=True)
             if hooks and i in hooks:
                 hooks[i]()
-        norm("norm", buf.out)
+            if i == DEPTH - 1:
+                norm("norm", buf.out)
+            yield
 
-    def _vit_blocks_folded(self, pre: str, buf: _ViTBuffers, M: int, hooks=None):
+    def _vit_blocks_folded(self, pre: str, buf: _ViTBuffers, M: int, hooks=None, sync=None):
         """The 24 Blocks with norm1 / norm2 folded across the GEMM boundary (dp_gemm_args.ln_*):
         `h` carries the un-normalised residual rows in 16 bits and `part` their 128-column chunk
         statistics, written by the producer (block 0: dp_layernorm_stats; then every proj / fc2
         epilogue beside its fp32 residual update); qkv / fc1 run on the folded weights
         (ops.fold_layernorm) and apply LN's per-row mean / rstd in their epilogue.  Same
         arithmetic as LN -> Linear up to where the 16-bit rounding falls (x instead of LN(x);
-        tools/ln_fold_emul.py: rel-L1 vs fp32 unchanged, 2.377e-3 vs 2.379e-3 bf16)."""
+        tools/ln_fold_emul.py: rel-L1 vs fp32 unchanged, 2.377e-3 vs 2.379e-3 bf16).  A generator
+        like _vit_steps."""
         P = self.P
         n_img = M // TOK
+        sync = sync or (lambda what, i: None)
         ops.layernorm_stats(buf.x, buf.h, buf.part, M, D)
+        yield
         for i in range(DEPTH):
             b = f"{pre}blocks.{i}."
+            sync("qkv", i)
             ops.gemm(buf.h, P[b + "attn.qkv.fold.w"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.fold.b"],
                      ln_in=(buf.part, P[b + "attn.qkv.fold.s"]))
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
+            sync("proj", i)
             ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
                      gamma=P[b + "ls1.gamma"], accumulate=True, ln_out=(buf.h, buf.part))
+            sync("fc1", i)
             ops.gemm(buf.h, P[b + "mlp.fc1.fold.w"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.fold.b"],
                      act=DP_ACT_GELU, ln_in=(buf.part, P[b + "mlp.fc1.fold.s"]))
             last = i == DEPTH - 1    # the final norm reads x itself
+            sync("fc2", i)
             ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
                      gamma=P[b + "ls2.gamma"], accumulate=True, ln_out=None if last else (buf.h, buf.part))
             if hooks and i in hooks:
                 hooks[i]()
-        ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
+            if last:
+                ops.layernorm(buf.x, P[pre + "norm.weight"], P[pre + "norm.bias"], buf.out, M, D)
+            yield
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
@@ -552,8 +582,14 @@ class Engine:
     def _side_encoders(self):
         """Image encoder ViT on x2 (encoder.py:308-311) and FOV encoder ViT (fov.py:66-72) as one
         grouped ViT, then the lowres upsample into `cat` and the FOV Linear (fov.py:45-47)."""
+        for _ in self._side_steps():
+            pass
+
+    def _side_steps(self):
+        """_side_encoders as a generator: the embedding, then one step per Block (the final norm
+        with the last), then the lowres upsample + FOV Linear after the last yield."""
         P, e = self.P, "encoder."
-        self._vit(self.side_vits, self.vs, 1, 34 * PTOK)
+        yield from self._vit_steps(self.side_vits, self.vs, 1, 34 * PTOK)
         ops.merge_windows(self.vi.out, 0, 1, 0, self.g)
         self._deconv(self.g, 24, D, P[e + "upsample_lowres.w"], self.cat, D, bias=P[e + "upsample_lowres.b"],
                      C_off=D, ldc=2 * D)
@@ -606,15 +642,44 @@ class Engine:
 
         # pyramid + 35 windows + patch-embed im2col (encoder.py:151-263)
         ops.patchify_pyramid(self.x0, self.cols)
-        # image and FOV encoders (one grouped ViT, M = 2 x 577 rows) beside the patch encoder
-        if side_ok:
+        # image and FOV encoders (one grouped ViT, M = 2 x 577 rows) beside the patch encoder:
+        # free-running on the side stream, or (side_gate = (R, J)) side block k released when the
+        # patch encoder reaches point R of its block k and joined before the next point J, so that
+        # side workgroups land only in chosen launches (points: qkv < proj < fc1 < fc2 of a block)
+        gate = self.side_gate if side_ok and not serial else None
+        sync = None
+        if side_ok and not gate:
             with self._on(self.side):
                 self._side_encoders()
+        elif gate:
+            steps = self._side_steps()
+            with self._on(self.side):
+                next(steps)                         # the side embedding (after patchify)
+            order = ("qkv", "proj", "fc1", "fc2")
+            rel, join = gate
+            pending = []
+
+            def sync(what, i):
+                if pending and what == join and (i > pending[0][0] or order.index(join) > order.index(rel)):
+                    main.wait_event(pending.pop(0)[1])
+                if what == rel:                     # main has issued everything before this point
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                    self.side.wait_event(ev)
+                    with _StreamCtx(self.side):
+                        next(steps)                 # side block i
+                    done = torch.cuda.Event()
+                    done.record(self.side)
+                    pending.append((i, done))
         # patch encoder; hooks after blocks 5 / 11 (encoder.py:133-144, 267-288)
         vp = self.vp
         hooks = {5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
                  11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1)}
-        self._vit(["encoder.patch_encoder."], vp, NWIN, 0, hooks)
+        self._vit(["encoder.patch_encoder."], vp, NWIN, 0, hooks, sync)
+        if gate:
+            with _StreamCtx(self.side):
+                for _ in steps:                     # the side encoders' tail (lowres upsample, FOV Linear)
+                    pass
         ops.merge_windows(vp.out, 0, 5, 3, self.f0)
         ops.merge_windows(vp.out, 25, 3, 6, self.f1)
         ops.merge_windows(vp.out, 34, 1, 0, self.f2)

@@ -30,21 +30,29 @@ def dtype_code(dt: torch.dtype) -> int:
     raise _lib.DPError(f"unsupported dtype {dt}")
 
 
-# Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, shape, dtype, ev0, ev1).
+# Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, shape, dtype, ev0, ev1, stream).
 _PROF: Optional[list] = None
+_PROF_T0: Optional[torch.cuda.Event] = None
 
 
 def profile_begin() -> None:
-    global _PROF
+    global _PROF, _PROF_T0
     _PROF = []
+    _PROF_T0 = torch.cuda.Event(enable_timing=True)
+    _PROF_T0.record()
 
 
-def profile_end() -> list:
-    """Stop recording; returns [(kind, flops, shape, operand dtype, milliseconds)] (synchronizes)."""
+def profile_end(timeline: bool = False) -> list:
+    """Stop recording; returns [(kind, flops, shape, operand dtype, milliseconds)] (synchronizes).
+    timeline=True: [(kind, flops, shape, dtype, start ms, end ms, stream)] relative to
+    profile_begin on the current stream (events of every stream share the device clock)."""
     global _PROF
     rec, _PROF = _PROF or [], None
     torch.cuda.synchronize()
-    return [(k, f, sh, dt, a.elapsed_time(b)) for (k, f, sh, dt, a, b) in rec]
+    if timeline:
+        return [(k, f, sh, dt, _PROF_T0.elapsed_time(a), _PROF_T0.elapsed_time(b), st)
+                for (k, f, sh, dt, a, b, st) in rec]
+    return [(k, f, sh, dt, a.elapsed_time(b)) for (k, f, sh, dt, a, b, st) in rec]
 
 
 class _Timed:
@@ -61,7 +69,8 @@ class _Timed:
     def __exit__(self, *exc):
         if _PROF is not None:
             self.e1.record()
-            _PROF.append((self.kind, self.flops, self.shape, self.dtype, self.e0, self.e1))
+            _PROF.append((self.kind, self.flops, self.shape, self.dtype, self.e0, self.e1,
+                          torch.cuda.current_stream().cuda_stream))
         return False
 
 

@@ -62,13 +62,36 @@ def raw_depth_u16(depth_np: np.ndarray) -> np.ndarray:
     return ((depth_np - min_depth) / (max_depth - min_depth) * 65535).astype(np.uint16)
 
 
-def _write_png(path: str, arr: np.ndarray) -> None:
-    from PIL import Image
+def _png_bytes(arr: np.ndarray, level: int = 1) -> bytes:
+    """PNG file bytes of an 8-bit RGB (H, W, 3) or 16-bit greyscale (H, W) image: filter type 0
+    on every row and one zlib stream (level 1) -- the same pixels as any PNG writer (the
+    reference's cv2.imwrite included), ~3x faster than PIL's adaptive filtering, and zlib runs
+    without the GIL, so writer threads scale."""
+    import struct
+    import zlib
 
-    if arr.dtype == np.uint16:
-        Image.fromarray(np.ascontiguousarray(arr)).save(path)          # 16-bit greyscale (I;16)
+    if arr.dtype == np.uint16 and arr.ndim == 2:
+        depth, ctype, rows = 16, 0, arr.astype(">u2").view(np.uint8).reshape(arr.shape[0], -1)
+    elif arr.dtype == np.uint8 and arr.ndim == 3 and arr.shape[2] == 3:
+        depth, ctype, rows = 8, 2, arr.reshape(arr.shape[0], -1)
     else:
-        Image.fromarray(np.ascontiguousarray(arr)).save(path, compress_level=1)
+        raise ValueError(f"_png_bytes: unsupported image {arr.dtype} {arr.shape}")
+    h, w = arr.shape[0], arr.shape[1]
+    raw = np.empty((h, rows.shape[1] + 1), np.uint8)
+    raw[:, 0] = 0
+    raw[:, 1:] = rows
+
+    def chunk(tag: bytes, data: bytes) -> bytes:
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+    ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)
+    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", zlib.compress(raw.tobytes(), level)) +
+            chunk(b"IEND", b""))
+
+
+def _write_png(path: str, arr: np.ndarray) -> None:
+    with open(path, "wb") as f:
+        f.write(_png_bytes(np.ascontiguousarray(arr)))
 
 
 _MODEL = {}
@@ -210,7 +233,7 @@ def plan_frames(image_paths, output_dir: str, world: int, rank: int, resume: boo
 
 
 def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_factor=1.0, half_precision=False,
-                              colored=True, cmap="turbo", decode_workers=4, encode_workers=4, pointcloud=False,
+                              colored=True, cmap="turbo", decode_workers=4, encode_workers=None, pointcloud=False,
                               resume=False, model=None):
     """Directory loop (reference :153-206), pipelined decode -> GPU -> encode, frame-sharded across ranks.
 
@@ -233,6 +256,8 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
     if model is None:
         model = _model(_device(), half_precision)
     model, transform = model
+    if encode_workers is None:   # PNG (+ PLY) writing is the host side's long pole: zlib drops the GIL
+        encode_workers = max(4, min(8, len(os.sched_getaffinity(0)) // 2))
 
     successful = 0
     t0 = time.time()

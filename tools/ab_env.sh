@@ -1,5 +1,5 @@
 #!/bin/bash
-# In-frame A/B of environment settings (product switches such as DP_LN_FOLD=0), alternating,
+# In-frame A/B of environment settings (bench.py AB_KNOBS such as DP_LN_FOLD=0), alternating,
 # 2 rounds, bench.py lines into gpurun_out/<tag>/ (run on the gpurun box from the repo root).
 # Usage: tools/ab_env.sh <tag> "VAR=a" "VAR=b" ...
 set -eo pipefail
@@ -10,8 +10,7 @@ for R in 1 2; do
   i=0
   for E in "$@"; do
     i=$((i + 1))
-    AB=""; case "$E" in *DP_GEMM_DEBUG*|*DP_ABLATE*) AB="--ab" ;; esac
-    env $E timeout -k 10 300 python -u bench.py $AB --no-cpu-baseline --steps 40 > $OUT/ab_${i}_$R.json 2> $OUT/ab_${i}_$R.err
+    env $E timeout -k 10 300 python -u bench.py --ab --no-cpu-baseline --steps 40 > $OUT/ab_${i}_$R.json 2> $OUT/ab_${i}_$R.err
   done
 done
 python - "$OUT" "$@" <<'PY'
