@@ -55,6 +55,17 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t dst) {
       : "v"(src), "s"(dst)
       : "memory");
 }
+// the same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset
+// (saddr form): a full tile's addresses are one scalar add away from the last tile's
+__device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, uint32_t dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(dst)
+      : "memory");
+}
 
 // Running max (m_run, log2 units), set exactly by the first 32-key half tile only; every
 // later score is taken as P = 2^(s sl2 - m_run) with no max pass, no compare and no rescale.
@@ -129,16 +140,30 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   // (finite, masked to -inf / weight 0 in the partial tile).
   const int prow = wave * 8 + (lane >> 3), pslot = lane & 7;
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(&smem[0][0]) + wave * 1024);
-  auto issue = [&](int k0, int buf) __attribute__((always_inline)) {
+  // full tiles: per-lane byte offsets of the K / V pieces from the tile's first key row (rows
+  // prow and prow + 32 share the swizzle) off a wave-uniform tile base; the partial tile clamps
+  // its rows past seq to row seq-1 (64-bit per-lane addresses)
+  const uint32_t voff_k = (uint32_t)(2 * (prow * ldq + kcol + 8 * (pslot ^ ((prow >> 1) & 7))));
+  const uint32_t voff_v = (uint32_t)(2 * (prow * ldq + vcol + 8 * (pslot ^ (((prow >> 1) & 1) << 2))));
+  auto issue = [&](int k0, int buf, auto full_tag) __attribute__((always_inline)) {
     if (ABL(8)) return;
     const uint32_t dk = __builtin_amdgcn_readfirstlane(lds0 + buf * 2 * TILE_B), dv = dk + TILE_B;
-    #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = prow + 32 * i;
-      const int key = min(k0 + row, seq - 1);
-      const u16* r = base + (long long)key * ldq;
-      glds16(r + kcol + 8 * (pslot ^ ((row >> 1) & 7)), dk + i * 4096);
-      glds16(r + vcol + 8 * (pslot ^ (((row >> 1) & 1) << 2)), dv + i * 4096);
+    if constexpr (decltype(full_tag)::value) {
+      const u16* r0 = base + (long long)k0 * ldq;
+      const u16* r1 = r0 + 32 * ldq;
+      glds16s(voff_k, r0, dk);
+      glds16s(voff_v, r0, dv);
+      glds16s(voff_k, r1, dk + 4096);
+      glds16s(voff_v, r1, dv + 4096);
+    } else {
+      #pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = prow + 32 * i;
+        const int key = min(k0 + row, seq - 1);
+        const u16* r = base + (long long)key * ldq;
+        glds16(r + kcol + 8 * (pslot ^ ((row >> 1) & 7)), dk + i * 4096);
+        glds16(r + vcol + 8 * (pslot ^ (((row >> 1) & 1) << 2)), dv + i * 4096);
+      }
     }
   };
   // transposed V read address (bytes, within a stage) for the A operand of
@@ -314,18 +339,27 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
     #pragma unroll
     for (int i = 0; i < 4; ++i) ls4[i] = 0.f;
     m_run = -INFINITY;
-    if (nmma > 0) issue(0, 0);
+    if (nfull > 0) issue(0, 0, std::true_type{});
+    else if (nmma > 0) issue(0, 0, std::false_type{});
     // top of tile t: tile t landed (own pieces: vmcnt(0); everyone's: the barrier, which also
     // frees the stage of tile t-1 for the next issue)
     auto top = [&](int t) __attribute__((always_inline)) {
       if (!ABL(4) && !ABL(8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      if (t + 1 < nmma) issue((t + 1) * KT, stage_of(t + 1));
+      if (t + 1 < nfull) issue((t + 1) * KT, stage_of(t + 1), std::true_type{});
+      else if (t + 1 < nmma) issue((t + 1) * KT, stage_of(t + 1), std::false_type{});
     };
     if (nfull > 0) {
       top(0);
       do_tile(0, std::false_type{}, true, exact);
     }
-    for (int t = 1; t < nfull; ++t) {
+    // the steady loop: the next tile is a full one (scalar tile base + lane offsets)
+    int t = 1;
+    for (; t + 1 < nfull; ++t) {
+      if (!ABL(4) && !ABL(8)) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      issue((t + 1) * KT, stage_of(t + 1), std::true_type{});
+      do_tile(t, std::false_type{}, false, exact);
+    }
+    if (t < nfull) {
       top(t);
       do_tile(t, std::false_type{}, false, exact);
     }

@@ -4,6 +4,7 @@
 namespace dpg {
 int launch_part_big(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s) {
   switch (tile) {
+    case TILE_GRP_128x128: return (bf16 ? launch_big<KBF16, 128, 128, 64, 3, true>(p, conv, s) : launch_big<KF16, 128, 128, 64, 3, true>(p, conv, s));
     case DP_TILE_BIG_256x128: return (bf16 ? launch_big<KBF16, 256, 128, 64, 3, true>(p, conv, s) : launch_big<KF16, 256, 128, 64, 3, true>(p, conv, s));
     case DP_TILE_BIG_256x128_K32: return (bf16 ? launch_big<KBF16, 256, 128, 32, 6, true>(p, conv, s) : launch_big<KF16, 256, 128, 32, 6, true>(p, conv, s));
     case DP_TILE_BIG_256x256_K32: return (bf16 ? launch_big<KBF16, 256, 256, 32, 2, false>(p, conv, s) : launch_big<KF16, 256, 256, 32, 2, false>(p, conv, s));

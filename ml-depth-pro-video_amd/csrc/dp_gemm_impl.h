@@ -102,6 +102,7 @@ int num_cus();
 
 // Engine families, one translation unit each: launch `p` (planned by dp_gemm.hip) on `tile`.
 int launch_part_big(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);      // dp_gemm_big.hip
+constexpr int TILE_GRP_128x128 = -1;   // internal: the grouped (side-encoder) launches' 128 x 128 big tile
 int launch_part_big320(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);   // dp_gemm_big320.hip
 int launch_part_8ph(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);      // dp_gemm_8ph.hip
 int launch_part_8ph320(const GemmP& p, bool conv, bool bf16, hipStream_t s);             // dp_gemm_8ph320.hip
@@ -2806,11 +2807,11 @@ int launch_big(const GemmP& p0, bool conv, hipStream_t s) {
   // engines the planner picks; debug 1 << 20: always the general one (A/B)
   const int ea = BKT == 64 ? fast_epi_act(p) : -1;
   if (p.groups > 1) {
-    // grouped launches (the side encoders' dense GEMMs) exist for the 256 x 128 dense engine only
-    if constexpr (BM == 256 && BN == 128 && BKT == 64 && NS == 3 && PIPE) {
+    // grouped launches (the side encoders' dense GEMMs) exist for the 256 x 128 / 128 x 128 dense engines
+    if constexpr ((BM == 256 || BM == 128) && BN == 128 && BKT == 64 && NS == 3 && PIPE) {
       if (conv || p.relu_a) return DP_ERR_ARG;
       dim3 g(p.tiles_n * p.tiles_m * p.groups);
-#define DP_GRP(E_) hipLaunchKernelGGL((gemm_big_kernel<K_, 256, 128, 64, 3, true, false, false, 8, E_, true>), g, dim3(NT_BIG), 0, s, p)
+#define DP_GRP(E_) hipLaunchKernelGGL((gemm_big_kernel<K_, BM, BN, 64, 3, true, false, false, 8, E_, true>), g, dim3(NT_BIG), 0, s, p)
       if (ea == DP_ACT_NONE) DP_GRP(DP_ACT_NONE);
       else if (ea == DP_ACT_GELU) DP_GRP(DP_ACT_GELU);
       else if (ea == EPI_ACC) DP_GRP(EPI_ACC);

@@ -13,13 +13,4 @@ for R in 1 2; do
     env $E timeout -k 10 300 python -u bench.py --ab --no-cpu-baseline --steps 40 > $OUT/ab_${i}_$R.json 2> $OUT/ab_${i}_$R.err
   done
 done
-python - "$OUT" "$@" <<'PY'
-import json, sys, glob
-out, envs = sys.argv[1], sys.argv[2:]
-for i, e in enumerate(envs, 1):
-    for f in sorted(glob.glob(f"{out}/ab_{i}_*.json")):
-        d = json.loads(open(f).read().strip().splitlines()[-1])
-        dk = d["roofline"]["dominant_kernel"]
-        v = d["value"] if d.get("value") is not None else d.get("ab_fps")
-        print(e, f.split("/")[-1], v, d["ms_per_step"], d["parity"]["depth_rel_l1"], dk["kind"], dk["avg_us"])
-PY
+python tools/ab_summary.py "$OUT" "$@" | tee $OUT/ab.txt
