@@ -37,7 +37,8 @@ def main():
     ap.add_argument("--size", default="1536x1536", help="WxH of the input frames")
     ap.add_argument("--pointcloud", action="store_true")
     ap.add_argument("--raw", action="store_true")
-    ap.add_argument("--workers", type=int, default=4, help="decode and encode threads each")
+    ap.add_argument("--workers", type=int, default=None,
+                    help="decode and encode threads each (default: the loop's own defaults)")
     ap.add_argument("--dir", default=None, help="scratch directory (default: a temp dir, removed)")
     args = ap.parse_args()
     W, H = (int(v) for v in args.size.split("x"))
@@ -65,8 +66,13 @@ def main():
     m, transform = model
     torch.cuda.synchronize()
     t_setup = time.time() - t
-    kw = dict(colored=not args.raw, pointcloud=args.pointcloud, decode_workers=args.workers,
-              encode_workers=args.workers, model=model)
+    kw = dict(colored=not args.raw, pointcloud=args.pointcloud, model=model)
+    if args.workers:
+        kw.update(decode_workers=args.workers, encode_workers=args.workers)
+    import inspect
+    dflt = inspect.signature(G.batch_generate_depth_maps).parameters
+    n_dec = kw.get("decode_workers", dflt["decode_workers"].default)
+    n_enc = kw.get("encode_workers") or max(4, min(8, len(os.sched_getaffinity(0)) // 2))
     # warm-up pass over 2 frames (first launches, allocator, thread pools), then the timed loop
     warm = os.path.join(root, "warm")
     os.makedirs(warm, exist_ok=True)
@@ -82,7 +88,7 @@ def main():
     paths = sorted(os.path.join(src, f) for f in os.listdir(src))
     # stage: decode alone (the loop's decoder: depth_pro.load_rgb in a pool)
     t = time.time()
-    with ThreadPoolExecutor(args.workers) as ex:
+    with ThreadPoolExecutor(n_dec) as ex:
         imgs = list(ex.map(lambda p: G._load(p, 1.0)[0], paths))
     t_dec = time.time() - t
     # stage: GPU alone (transform + infer on host frames already decoded; includes the u8 upload)
@@ -102,7 +108,7 @@ def main():
     hosts = [G._image_async(d, not args.raw, "turbo") for d in depths]
     torch.cuda.synchronize()
     t = time.time()
-    with ThreadPoolExecutor(args.workers) as ex:
+    with ThreadPoolExecutor(n_enc) as ex:
         list(ex.map(lambda ih: G._write_png(os.path.join(root, f"enc_{ih[0]}.png"), G._host_image(ih[1])),
                     enumerate(hosts)))
     t_enc = (time.time() - t) / len(hosts)
@@ -120,7 +126,7 @@ def main():
     out = {
         "what": "generate_depth_maps.batch_generate_depth_maps end to end, 1 GPU",
         "frames": args.frames, "size": [W, H], "pointcloud": args.pointcloud, "raw": args.raw,
-        "workers": args.workers, "frames_ok": n_ok,
+        "decode_workers": n_dec, "encode_workers": n_enc, "frames_ok": n_ok,
         "loop_fps": round(args.frames / t_loop, 2),
         "stage_fps": {"decode_png_pool": round(len(paths) / t_dec, 2),
                       "gpu_infer_incl_upload": round(1.0 / t_gpu, 2),
