@@ -50,7 +50,7 @@ def tile_kernel(tile: int, dtype: torch.dtype) -> str:
 
 # The PMC traffic summary the bench line cites (tools/pmc_traffic.py over separate FETCH_SIZE /
 # WRITE_SIZE passes of the tree being benched); named explicitly, updated with each profiled tree.
-PMC_TRAFFIC = "profiles/r03ac_pmc_traffic.json"
+PMC_TRAFFIC = "profiles/r04_pmc_traffic.json"
 
 
 def pmc_traffic(kernel: str, workgroups: int):
