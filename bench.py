@@ -4,9 +4,10 @@
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-A step = every rank runs `DepthPro.infer` on one synthetic 1536x1536 frame that
-is already resident in HBM (u8 -> normalise -> hipGraph forward -> depth
-epilogue), and (N > 1) the depth maps are gathered to rank 0 over RCCL.
+A step = every rank runs `DepthPro.infer(transform(frame))` on one synthetic 1536x1536
+uint8 frame that is already resident in HBM (transform: u8 -> normalised fp32 on the GPU;
+infer: copy into the engine input -> hipGraph forward -> depth epilogue -> frame status), and
+(N > 1) the depth maps are gathered to rank 0 over RCCL.
 Weights: synthetic seed-0 set (no checkpoint offline), packed once on rank 0
 and RCCL-broadcast.  Prints ONE JSON line on rank 0.
 """
@@ -82,7 +83,9 @@ def rocprof_avg_us(kernel: str):
         rows = list(csv.DictReader(open(path)))
     except OSError:
         return None
-    hit = [r for r in rows if r["Name"].startswith("void " + kernel) or r["Name"].startswith(kernel)]
+    def bare(name):   # "void (anonymous namespace)::gemm_p8ph_kernel<...>(dpg::GemmP)" -> "gemm_p8ph_kernel<...>..."
+        return name.replace("void ", "", 1).replace("(anonymous namespace)::", "")
+    hit = [r for r in rows if bare(r["Name"]).startswith(kernel)]
     if not hit:
         return None
     calls = sum(int(r["Calls"]) for r in hit)
@@ -227,8 +230,8 @@ def main():
     import depth_pro
     from depth_pro import distributed as D
     from depth_pro import ops
-    from depth_pro.depth_pro import DepthPro, DepthProConfig, _compute_dtype
-    from depth_pro.engine import Engine, pack_weights
+    from depth_pro.depth_pro import DepthPro, DepthProConfig, Transform, _compute_dtype
+    from depth_pro.engine import pack_weights
     from depth_pro.weights import synthetic_state_dict
 
     t_setup = time.time()
@@ -240,7 +243,10 @@ def main():
         packed = D.broadcast_packed(packed, dev, src=0)
     else:
         packed = pack_weights(synthetic_state_dict(0), dev, code)
-    eng = Engine(packed, dev, code)
+    # the drop-in API object (depth_pro.DepthPro), on the packed weight set (rank 0's, broadcast)
+    model = DepthPro.from_packed(packed, dev, code)
+    transform = Transform(dev, torch.float32)
+    eng = model.engine()
     if not args.no_graph:
         eng.capture_graph()
     torch.cuda.synchronize()
@@ -248,36 +254,33 @@ def main():
 
     # resident inputs: this rank's first `pool` frames of the stream (frame k -> rank k mod N), u8 in HBM
     frames = [torch.from_numpy(frame(k)).to(dev) for k in D.shard_frames(args.pool * world, rank, world)]
-    # two depth buffers: frame i's gather to rank 0 (RCCL, its own stream) runs while
-    # frame i+1 computes; the buffer is reused only after its gather's work.wait()
-    depths = [torch.empty(1536, 1536, dtype=torch.float32, device=dev) for _ in range(2)]
-    depth = depths[0]
-    fpx = torch.empty((), dtype=torch.float32, device=dev)
+    # frame i's depth map goes to rank 0 by an asynchronous RCCL gather (its own stream) while
+    # frame i+1 computes; the depth tensor stays referenced until that gather's work.wait()
     pending = [None, None]
 
     counter = [0]
-    statuses = []          # FrameStatus of every frame this rank ran (checked after the timed loop)
+    statuses = []          # BatchStatus of every infer call this rank made (checked after the timed loop)
 
     def step(i):
-        d = depths[i & 1]
         if pending[i & 1] is not None:
-            pending[i & 1].wait()
+            pending[i & 1][1].wait()
             pending[i & 1] = None
         n = counter[0]
         counter[0] += 1
-        # DepthPro.infer's device work for a resident frame: normalise, forward, epilogue with the
-        # frame's health word, the asynchronous status snapshot (engine.FrameStatus)
-        ops.normalize_u8(frames[n % len(frames)], eng.x0)
-        c, fov = eng.run()
-        ops.infer_epilogue(c, fov, None, 1536, 1536, d, fpx, eng.status_dev[-1:])
-        statuses.append(eng.finish_status())
+        # the user's call: transform (u8 -> normalised fp32 on the GPU) + DepthPro.infer (copy into
+        # the engine input, graph replay of the forward, depth / focal-length epilogue, status)
+        with torch.no_grad():
+            pred = model.infer(transform(frames[n % len(frames)]))
+        statuses.append(model.last_status())
         if world > 1:
-            _, pending[i & 1] = D.gather_frames(d, dst=0, async_op=True)
+            d = pred["depth"]
+            _, work = D.gather_frames(d, dst=0, async_op=True)
+            pending[i & 1] = (d, work)
 
     def drain():
         for j in range(2):
             if pending[j] is not None:
-                pending[j].wait()
+                pending[j][1].wait()
                 pending[j] = None
 
     for i in range(args.warmup):
@@ -308,8 +311,8 @@ def main():
     # every benched frame healthy: no timed-out stream-K hand-off, depth / focal length all finite
     bad = [st for st in statuses if st.error() is not None]
     if bad and not args.ab:
-        refuse(f"rank {rank}: {len(bad)} of {len(statuses)} benched frames invalid "
-               f"(first: frame {bad[0].frame}: {bad[0].error()})", 5)
+        refuse(f"rank {rank}: {len(bad)} of {len(statuses)} benched infer calls invalid "
+               f"(first: {bad[0].error()})", 5)
 
     # per-kernel roofline leg: one instrumented eager frame in the same stream layout as the
     # captured graph (side encoders and decoder chains concurrent, so a launch sees the CUs the
@@ -331,14 +334,15 @@ def main():
 
     parity = None
     if rank == 0:
-        ops.normalize_u8(frames[0], eng.x0)
-        c, fov = eng.run()
-        ops.infer_epilogue(c, fov, None, 1536, 1536, depth, fpx, eng.status_dev[-1:])
-        eng.finish_status()
+        # frame 0 through the API (graph replay) against the reference's output
+        x = transform(frames[0])
+        with torch.no_grad():
+            c, fov = model.forward(x.unsqueeze(0))
+            depth = model.infer(x)["depth"]
         torch.cuda.synchronize()
         parity = depth_parity(depth, c, fov)
         if not args.ab:
-            eng.check_status(block=True)
+            model.last_status().check()
         if parity is None:
             refuse("tests/golden/golden_forward_frame0.npz missing: depth L1 vs reference not measurable", 4)
         if not args.ab and not parity["depth_rel_l1"] < parity["target"]:
