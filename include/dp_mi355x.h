@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 10
+#define DP_ABI_VERSION 11
 int dp_abi_version(void);
 
 /*
@@ -146,7 +146,8 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
        DP_TILE_DEEP5_256x256 = 10, DP_TILE_DEEP_256x128 = 11, DP_TILE_STREAMK_256x256 = 12,
        DP_TILE_BIG_320x256 = 13, DP_TILE_BIG_512x128 = 14, DP_TILE_PBIG_320x256 = 15,
        DP_TILE_PBIG_256x256 = 16, DP_TILE_DUAL_256x128 = 17,
-       DP_TILE_P8PH_256x256 = 18, DP_TILE_8PH_320x256 = 19, DP_TILE_CV3_256x256 = 20 };
+       DP_TILE_P8PH_256x256 = 18, DP_TILE_8PH_320x256 = 19, DP_TILE_CV3_256x256 = 20,
+       DP_TILE_SPLITK_256x256 = 21 };
 /* DP_TILE_P8PH_256x256: persistent 8-phase engine (min(tiles, CUs) workgroups, each a stream of
    K steps over its tiles; dense A, N % 256 == 0, K >= 128, 16-bit C without per-row operands);
    the auto choice for the ViT fc1.  DP_TILE_8PH_320x256: 8-phase 320 x 256 engine (dense A, no
@@ -155,7 +156,12 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
    serve returns DP_ERR_ARG.  DP_TILE_CV3_256x256: stride-1 pad-1 3x3 implicit conv on 16 x 16 pixel
    tiles with the input patch in LDS (square maps, side % 16 == 0, in_c % 64 == 0; N % 256 == 0 with
    ReLU / residual epilogues, or N % 128 == 0 with head_corr, or DP_STORE_HEAD_PS); the auto choice
-   for the many-round ResidualBlock convs and the border-corrected composed conv at 768^2. */
+   for the many-round ResidualBlock convs and the border-corrected composed conv at 768^2.
+   DP_TILE_SPLITK_256x256 (ABI 11, needs a workspace, not selectable as a hint): split-K for small
+   grids -- the 256 x 256 tiles' K steps split over up to (CUs / tiles) workgroups that write fp32
+   partials into the workspace, then a reduce launch sums them in split order and runs the
+   epilogue (DP_STORE_ROWS, no row groups / head); the auto choice for long-K GEMMs with fewer
+   than a third as many tiles as CUs (the decoder's 48^2 / 96^2 convs and projections). */
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 

@@ -132,6 +132,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   const long long tiles256 = (long long)((a->M + 255) / 256) * (a->N / 256);
   if (tile == DP_TILE_STREAMK_256x256 && (!ws_ok || a->N % 256 != 0)) return DP_ERR_ARG;
+  if (tile == DP_TILE_SPLITK_256x256) return DP_ERR_ARG;   // chosen by the planner only (it sizes the split)
   if (tile == DP_TILE_AUTO) {
     if (a->N <= 32) tile = DP_TILE_256x32;
     else if (a->N <= 64) tile = DP_TILE_256x64;
@@ -147,7 +148,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     }
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
     else if (ws_ok && a->a_mode == DP_A_CONV && !(dbg & 32) && tiles256 < num_cus() &&
-             a->K >= 4608) {
+             (a->K >= 4608 || ((dbg & (1 << 27)) && a->K >= 2304 && tiles256 >= 128) ||
+              ((dbg & (1 << 28)) && a->K >= 2304 && tiles256 >= 32))) {
       // Implicit convs with fewer 256 x 256 tiles than CUs and K >= 4608 (the decoder's
       // 512/1024-channel projections at 48^2 - 192^2) on the stream-K engine, each
       // tile's K range split (sk_grid): 153 -> 108, 152 -> 112, 152 -> 126 us in-frame
@@ -187,6 +189,24 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       // 16384 -> 256 x 256 (both persistent below when eligible)
       if (tile == DP_TILE_8PH_256x256 && (dbg & 8192)) tile = DP_TILE_BIG_320x256;
       else if (tile == DP_TILE_8PH_256x256 && (dbg & 16384)) tile = DP_TILE_BIG_256x256;
+    }
+  }
+  // split-K for small grids of long-K GEMMs (the decoder's 48^2 / 96^2 convs and projections,
+  // fuse_lowres): with <= a third as many 256 x 256 tiles as CUs, each tile's K steps go to
+  // S = min(CUs / tiles, K steps / 2, workspace slabs, 32) workgroups, then one reduce launch
+  // (DP_TILE_SPLITK_256x256; debug 1 << 27: off)
+  int ksplit = 1;
+  if (a->tile == DP_TILE_AUTO && ws_ok && !(dbg & (1 << 27)) && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
+      !a->row_group && !a->head_w && !a->head_corr && !lnp && !lnc) {
+    const long long ncu = num_cus(), kt = a->K / BK;
+    const long long slab = (long long)a->M * a->N * 4;
+    long long sp = tiles256 > 0 ? ncu / tiles256 : 0;
+    if (sp > kt / 2) sp = kt / 2;
+    if (sp > (a->workspace_bytes - SK_FLAG_BYTES) / slab) sp = (a->workspace_bytes - SK_FLAG_BYTES) / slab;
+    if (sp > 32) sp = 32;
+    if (sp >= 3) {
+      tile = DP_TILE_SPLITK_256x256;
+      ksplit = (int)sp;
     }
   }
   // byte extent of C for the persistent engine's bounded buffer stores (0: not eligible)
@@ -302,6 +322,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   p.dbg = dbg;
   p.c_bytes = c_bytes;
+  p.ksplit = ksplit;
+  p.kpart = ksplit > 1 ? (float*)((char*)a->workspace + SK_FLAG_BYTES) : nullptr;
   p.groups = 1;
   p.stagger_wg = 0;
   p.stagger_sleeps = 0;
@@ -331,6 +353,7 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
   int grid = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   if (tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256 || tile == DP_TILE_P8PH_256x256)
     grid = grid < num_cus() ? grid : num_cus();
+  if (tile == DP_TILE_SPLITK_256x256) grid *= p.ksplit;
   if (grid_out) *grid_out = tile == DP_TILE_STREAMK_256x256 ? sk_grid(p) : grid;
   return 0;
 }
@@ -343,6 +366,7 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool conv = a->a_mode == DP_A_CONV;
   if (tile == DP_TILE_STREAMK_256x256) return launch_part_sk(p, conv, a->workspace, a->dtype == DP_BF16, s);
+  if (tile == DP_TILE_SPLITK_256x256) return launch_part_splitk(p, conv, a->dtype == DP_BF16, s);
   if (tile == DP_TILE_P8PH_256x256 && a->ln_part_in) {
     // folded-LN consumer on the persistent engine: merge each row's chunk statistics into
     // (rstd, -rstd * mean) in the workspace's first partial-tile slot (no stream-K launch uses

@@ -81,6 +81,11 @@ struct GemmP {
   // dp_gemm_grouped: `groups` problems of one shape in one launch (workgroup range g * tiles_m *
   // tiles_n ... covers problem g, whose operand pointers are grp[g]); 1 otherwise
   int groups;
+  // split-K (DP_TILE_SPLITK_256x256): workgroup range s * tiles ... covers K-steps [s KT / ksplit,
+  // (s+1) KT / ksplit) of every tile and stores raw fp32 partials into kpart + s M N; a reduce
+  // launch adds them and runs the epilogue; 1 otherwise
+  int ksplit;
+  float* kpart;
   struct Group {
     const u16* A;
     const u16* B;
@@ -110,6 +115,7 @@ int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s);       
 int launch_part_pbig(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);     // dp_gemm_pbig.hip
 int launch_part_small(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);    // dp_gemm_small.hip
 int launch_part_sk(const GemmP& p, bool conv, void* ws, bool bf16, hipStream_t s);       // dp_gemm_sk.hip
+int launch_part_splitk(const GemmP& p, bool conv, bool bf16, hipStream_t s);             // dp_gemm_splitk.hip
 }  // namespace dpg
 
 namespace {
@@ -1050,7 +1056,7 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
 // GRP: a dp_gemm_grouped launch -- the workgroup's problem (wgid / tiles per problem) supplies the
 // operand pointers.
 template <typename K_, int BM, int BN, int BKT, int NS, bool PIPE, bool CONV, bool RELU, int NW = 8, int EACT = -1,
-          bool GRP = false>
+          bool GRP = false, bool SPLIT = false>
 __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(const GemmP p_arg) {
   // 8 waves as WM x WN; the 512 x 128 tile (N = 128 layers) uses 4 x 2 so that every
   // wave still owns a 128 x 64 sub-tile (same fragment reuse as the 256 x 256 tile);
@@ -1091,7 +1097,23 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
     p_grp.A = q.A; p_grp.B = q.B; p_grp.bias = q.bias; p_grp.gamma = q.gamma; p_grp.pos = q.pos;
     p_grp.R1 = q.R1; p_grp.R2 = q.R2; p_grp.C = q.C;
   }
-  const GemmP& p = GRP ? p_grp : p_arg;
+  // split-K: this workgroup's K-step range and its fp32 partial slab as a plain C (no epilogue
+  // operands: the reduce launch applies them to the sum)
+  int kbeg = 0, kcnt = p_arg.K / BKT;
+  if constexpr (SPLIT) {
+    const int per = p_arg.tiles_m * p_arg.tiles_n;
+    const int sp = wgid / per;
+    wgid -= sp * per;
+    const int kt_all = p_arg.K / BKT;
+    kbeg = sp * kt_all / p_arg.ksplit;
+    kcnt = (sp + 1) * kt_all / p_arg.ksplit - kbeg;
+    p_grp = p_arg;
+    p_grp.C = p_arg.kpart + (long long)sp * p_arg.M * p_arg.N;
+    p_grp.ldc = p_arg.N; p_grp.c_dtype = DP_F32; p_grp.accumulate = 0; p_grp.store_mode = DP_STORE_ROWS;
+    p_grp.bias = nullptr; p_grp.gamma = nullptr; p_grp.pos = nullptr; p_grp.R1 = nullptr; p_grp.R2 = nullptr;
+    p_grp.act = DP_ACT_NONE; p_grp.row_group = 0; p_grp.head_w = nullptr; p_grp.head_corr = nullptr;
+  }
+  const GemmP& p = (GRP || SPLIT) ? p_grp : p_arg;
   int tile_m, tile_n;
   tile_coords(p, wgid, tile_m, tile_n);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
@@ -1124,7 +1146,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
   auto issue = [&](int kt, int stage) {
     const uint32_t sa = lds_base + stage * STAGE;
     const uint32_t sb = sa + A_BYTES;
-    const int k0 = kt * BKT;
+    const int k0 = (kt + kbeg) * BKT;
     int t_ky = 0, t_kx = 0, t_ci = 0;
     if constexpr (CONV) conv_tap(p, k0, t_ky, t_kx, t_ci);
     #pragma unroll
@@ -1190,7 +1212,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
     }
   };
 
-  const int KT = p.K / BKT;
+  const int KT = kcnt;
   auto nxt = [&](int st) { return st + 1 == NS ? 0 : st + 1; };
   // wait until tile t has landed: tiles issued so far are 0 .. min(KT-1, t+NS-2)
   auto wait_tile = [&](int t) { wait_vmcnt_le<(NS - 2) * LT>(min(NS - 2, KT - 1 - t) * LT); };
@@ -2639,6 +2661,65 @@ int launch_sk(const GemmP& p0, bool conv, void* ws, hipStream_t st) {
     else DP_SK(false, false, false);
   }
 #undef DP_SK
+  DP_CHECK_LAUNCH();
+  return 0;
+}
+
+// ========================================================== split-K (small grids, long K)
+// Launch 1: the 256 x 256 big engine over tiles x ksplit workgroups, each a K-step range of one
+// tile, raw fp32 partials into the workspace ([ksplit][M][N]); launch 2 (this kernel): every
+// thread sums the ksplit partials of 2 rows x 8 columns in split order (deterministic) and runs
+// the same row epilogue the engines use (bias, activation, gamma, pos, residuals, store mode).
+// No workgroup ever waits for another (unlike the stream-K hand-off), so a split-K launch can
+// run beside any other launch.
+template <typename K_>
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const GemmP p) {
+  const int cpr = p.N / 8;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long pairs = (p.M + 1) / 2;
+  if (idx >= pairs * cpr) return;
+  const int rp = (int)(idx / cpr), n = (int)(idx - (long long)rp * cpr) * 8;
+  int ms[2] = {2 * rp, 2 * rp + 1};
+  float v[2][8];
+  #pragma unroll
+  for (int it = 0; it < 2; ++it)
+    #pragma unroll
+    for (int r = 0; r < 8; ++r) v[it][r] = 0.f;
+  const long long slab = (long long)p.M * p.N;
+  const bool two = ms[1] < p.M;
+  const float* base = p.kpart + (long long)ms[0] * p.N + n;
+  #pragma unroll 4
+  for (int sp = 0; sp < p.ksplit; ++sp) {
+    const float* q = base + sp * slab;
+    const float4 a0 = *(const float4*)q, a1 = *(const float4*)(q + 4);
+    float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0;
+    if (two) { b0 = *(const float4*)(q + p.N); b1 = *(const float4*)(q + p.N + 4); }
+    v[0][0] += a0.x; v[0][1] += a0.y; v[0][2] += a0.z; v[0][3] += a0.w;
+    v[0][4] += a1.x; v[0][5] += a1.y; v[0][6] += a1.z; v[0][7] += a1.w;
+    v[1][0] += b0.x; v[1][1] += b0.y; v[1][2] += b0.z; v[1][3] += b0.w;
+    v[1][4] += b1.x; v[1][5] += b1.y; v[1][6] += b1.z; v[1][7] += b1.w;
+  }
+  ColConst cc;
+  load_colconst(p, n, cc);
+  epilogue_rows<K_, 2>(p, cc, ms, n, v);
+}
+
+template <typename K_>
+int launch_splitk(const GemmP& p0, bool conv, hipStream_t s) {
+  GemmP p = p0;
+  p.tiles_n = p.N / 256;
+  p.tiles_m = (p.M + 255) / 256;
+  if (p.ksplit < 2 || !p.kpart || p.N % 256 != 0) return DP_ERR_ARG;
+  dim3 g1(p.tiles_n * p.tiles_m * p.ksplit);
+#define DP_SPK(C_, R_) hipLaunchKernelGGL((gemm_big_kernel<K_, 256, 256, 64, 2, false, C_, R_, 8, -1, false, true>), g1, dim3(NT_BIG), 0, s, p)
+  if (conv && p.relu_a) DP_SPK(true, true);
+  else if (conv) DP_SPK(true, false);
+  else if (p.relu_a) DP_SPK(false, true);
+  else DP_SPK(false, false);
+#undef DP_SPK
+  DP_CHECK_LAUNCH();
+  const long long threads = (long long)((p.M + 1) / 2) * (p.N / 8);
+  hipLaunchKernelGGL(splitk_reduce_kernel<K_>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, p);
   DP_CHECK_LAUNCH();
   return 0;
 }

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 from depth_pro import ops  # noqa: E402
 from depth_pro._lib import (DP_ACT_GELU, DP_ACT_RELU, DP_TILE_8PH_256x256, DP_TILE_BIG_256x128,  # noqa: E402
                             DP_TILE_BIG_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_512x128,
-                            DP_TILE_DUAL_256x128, DP_TILE_STREAMK_256x256)
+                            DP_TILE_DUAL_256x128, DP_TILE_SPLITK_256x256, DP_TILE_STREAMK_256x256)
 
 DTYPES = [torch.bfloat16, torch.float16]
 
@@ -506,6 +506,66 @@ def test_gemm_stream_k_conv3x3_relu_residual(cuda, dt):
              relu_a=True, bias=b, R1=rh, ldr1=C, tile=DP_TILE_STREAMK_256x256, workspace=ops.gemm_workspace(cuda))
     ref = F.conv2d(F.relu(x.float()), w.float(), b, padding=1) + r.float()
     close(out.reshape(1, S, S, C).permute(0, 3, 1, 2), ref, dt, "stream-K conv3x3")
+
+
+SPLITK_CASES = [
+    # (name, M, N, K, conv side / None, mode)
+    ("rb conv 48^2 relu+res", 48 * 48, 256, 2304, 48, "rb"),
+    ("proj conv 96^2 1024ch", 96 * 96, 256, 9216, 96, "bias"),
+    ("dense ragged gelu", 2000, 512, 2048, None, "gelu"),
+    ("dense fp32 accumulate", 1500, 256, 4096, None, "acc"),
+]
+
+
+@pytest.mark.parametrize("case", SPLITK_CASES, ids=[c[0] for c in SPLITK_CASES])
+@pytest.mark.parametrize("dt", DTYPES)
+def test_gemm_split_k_matches_reference_and_data_parallel(cuda, dt, case):
+    """Split-K for small grids (DP_TILE_SPLITK_256x256, planner-chosen with a workspace): the 256 x
+    256 engine over K ranges writing fp32 partials, then the reduce launch with the row epilogue.
+    vs an fp32 reference, close to the data-parallel engine (only the fp32 summation order
+    differs), and bit-identical run to run (partials summed in split order)."""
+    name, M, N, K, S, mode = case
+    g = torch.Generator().manual_seed(M + N + K)
+    ws = ops.gemm_workspace(cuda)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    kw = dict(M=M, N=N, K=K, bias=bias)
+    if S is not None:
+        cin = K // 9
+        x = rnd(1, cin, S, S, dt=dt, dev=cuda, gen=g)
+        A = x.permute(0, 2, 3, 1).reshape(S * S, cin).contiguous()
+        w = B.float().cpu().reshape(N, cin // 64, 3, 3, 64).permute(0, 1, 4, 2, 3).reshape(N, cin, 3, 3)
+        kw["conv"] = dict(in_h=S, in_w=S, in_c=cin, k=3, stride=1, pad=1, out_h=S, out_w=S)
+        xin = F.relu(x.float()) if mode == "rb" else x.float()
+        ref = F.conv2d(xin, w.to(cuda), bias, padding=1).permute(0, 2, 3, 1).reshape(M, N)
+    else:
+        A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+        ref = A.float() @ B.float().t() + bias
+    if mode == "rb":
+        R = rnd(M, N, dt=dt, dev=cuda, gen=g)
+        kw.update(relu_a=True, R1=R, ldr1=N)
+        ref = ref + R.float()
+    if mode == "gelu":
+        kw.update(act=DP_ACT_GELU)
+        ref = F.gelu(ref)
+    if mode == "acc":
+        X = torch.randn(M, N, generator=g).to(cuda)
+        gamma = torch.rand(N, generator=g).to(cuda)
+        kw.update(gamma=gamma, accumulate=True)
+        ref = X + gamma * ref
+        C1, C2, C3 = X.clone(), X.clone(), X.clone()
+    else:
+        C1, C2, C3 = (torch.empty(M, N, dtype=dt, device=cuda) for _ in range(3))
+    tile, wgs = ops.gemm(A, B, C1, plan_only=True, workspace=ws, **kw)
+    assert tile == DP_TILE_SPLITK_256x256 and wgs > (M + 255) // 256 * (N // 256), (tile, wgs)
+    ops.gemm(A, B, C1, workspace=ws, **kw)
+    ops.gemm(A, B, C2, tile=DP_TILE_BIG_256x256, **kw)
+    ops.gemm(A, B, C3, workspace=ws, **kw)
+    torch.cuda.synchronize()
+    close(C1, ref, torch.float32 if (mode == "acc" and dt == torch.float16) else dt, f"split-K {name}")
+    d = (C1.float() - C2.float()).abs().max().item()
+    assert d <= 1e-2 * (C2.float().abs().max().item() + 1e-6), d
+    assert torch.equal(C1, C3)
 
 
 ENGINES = [DP_TILE_BIG_256x256, DP_TILE_8PH_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_256x128, DP_TILE_BIG_512x128,

@@ -14,7 +14,7 @@ from depth_pro._lib import (DP_TILE_128x128, DP_TILE_256x64, DP_TILE_8PH_256x256
                             DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128,
                             DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256)
 
-TILES = (("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
+TILES = (("auto", 0), ("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
          ("8ph256x256", DP_TILE_8PH_256x256), ("deep4_256x256", DP_TILE_DEEP4_256x256),
          ("deep5_256x256", DP_TILE_DEEP5_256x256), ("deep6_256x128", DP_TILE_DEEP_256x128),
          ("sk256x256", DP_TILE_STREAMK_256x256), ("big320x256", DP_TILE_BIG_320x256),
@@ -38,6 +38,12 @@ SHAPES = [  # (name, M, N, K, kw)
     ("conv3x3 192^2 256->256", 192 * 192, 256, 2304, {"conv": 192}),
     ("conv3x3 96^2 256->256", 96 * 96, 256, 2304, {"conv": 96}),
     ("conv3x3 48^2 256->256", 48 * 48, 256, 2304, {"conv": 48}),
+    # ResidualBlock second conv: ReLU prologue + residual epilogue (f16, as the decoder runs it)
+    ("rb conv 192^2", 192 * 192, 256, 2304, {"conv": 192, "rb": True}),
+    ("rb conv 96^2", 96 * 96, 256, 2304, {"conv": 96, "rb": True}),
+    ("rb conv 48^2", 48 * 48, 256, 2304, {"conv": 48, "rb": True}),
+    ("proj conv 48^2 1024->256", 48 * 48, 256, 9216, {"conv": 48}),
+    ("proj conv 96^2 1024->256", 96 * 96, 256, 9216, {"conv": 96}),
     ("head conv 768^2 256->128", 768 * 768, 128, 2304, {"conv": 768}),
     ("composed head 768^2 128->4x32", 768 * 768, 128, 1152, {"conv": 768}),
     ("deconv 384->768 256ch", 384 * 384, 1024, 256, {"deconv": (384, 384, 256)}),
@@ -79,6 +85,7 @@ def main():
     for name, M, N, K, kw in SHAPES:
         if args.only and args.only not in name:
             continue
+        dt = torch.float16 if kw.get("rb") or "proj conv" in name else torch.bfloat16
         B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
         bias = torch.randn(N, device=dev, generator=g)
         if "conv" in kw:
@@ -90,6 +97,7 @@ def main():
             A = torch.randn(M, K, device=dev, generator=g).to(dt)
             conv = None
         C = torch.zeros(M, N, device=dev, dtype=torch.float32 if kw.get("acc") else dt)
+        R1 = torch.randn(M, N, device=dev, generator=g).to(dt) if kw.get("rb") else None
         dc = kw.get("deconv")
         flop = 2.0 * M * N * K
         res = []
@@ -100,7 +108,8 @@ def main():
                 continue
             f = lambda: ops.gemm(A, B, C, M=M, N=N, K=K, conv=conv, bias=bias, act=2 if kw.get("gelu") else 0,
                                  accumulate=bool(kw.get("acc")), tile=tile, workspace=ws, deconv=dc,
-                                 ldc=dc[2] if dc else None)  # noqa: E731
+                                 ldc=dc[2] if dc else None, relu_a=bool(kw.get("rb")),
+                                 R1=R1, ldr1=N if R1 is not None else 0)  # noqa: E731
             ms = timeit(f, args.iters)
             res.append(f"{tname} {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
             if args.ablate and (tname.startswith("big") or tname.startswith("8ph") or tname.startswith("p8")
@@ -116,7 +125,7 @@ def main():
                 _lib.load().dp_gemm_debug_flags(args.dbg)
                 res.append("[" + " ".join(parts) + "]")
         # correctness of the big engine vs the small one on this shape
-        if not kw.get("acc") and not dc and not args.tile and not args.torch_only:
+        if not kw.get("acc") and not kw.get("rb") and not dc and not args.tile and not args.torch_only:
             C1 = torch.empty_like(C)
             ops.gemm(A, B, C1, M=M, N=N, K=K, conv=conv, bias=bias, tile=DP_TILE_128x128)
             C2 = torch.empty_like(C)
