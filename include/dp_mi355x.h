@@ -157,11 +157,10 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
    tiles with the input patch in LDS (square maps, side % 16 == 0, in_c % 64 == 0; N % 256 == 0 with
    ReLU / residual epilogues, or N % 128 == 0 with head_corr, or DP_STORE_HEAD_PS); the auto choice
    for the many-round ResidualBlock convs and the border-corrected composed conv at 768^2.
-   DP_TILE_SPLITK_256x256 (ABI 11, needs a workspace, not selectable as a hint): split-K for small
-   grids -- the 256 x 256 tiles' K steps split over up to (CUs / tiles) workgroups that write fp32
-   partials into the workspace, then a reduce launch sums them in split order and runs the
-   epilogue (DP_STORE_ROWS, no row groups / head); the auto choice for long-K GEMMs with fewer
-   than a third as many tiles as CUs (the decoder's 48^2 / 96^2 convs and projections). */
+   DP_TILE_SPLITK_256x256 (ABI 11, a hint only, needs a workspace): split-K for small grids -- the
+   256 x 256 tiles' K steps split over up to (CUs / tiles) workgroups that write fp32 partials into
+   the workspace, then a reduce launch sums them in split order and runs the epilogue
+   (DP_STORE_ROWS, no row groups / head); DP_ERR_SHAPE when no split of >= 2 fits. */
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 

@@ -132,7 +132,6 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   const long long tiles256 = (long long)((a->M + 255) / 256) * (a->N / 256);
   if (tile == DP_TILE_STREAMK_256x256 && (!ws_ok || a->N % 256 != 0)) return DP_ERR_ARG;
-  if (tile == DP_TILE_SPLITK_256x256) return DP_ERR_ARG;   // chosen by the planner only (it sizes the split)
   if (tile == DP_TILE_AUTO) {
     if (a->N <= 32) tile = DP_TILE_256x32;
     else if (a->N <= 64) tile = DP_TILE_256x64;
@@ -148,8 +147,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     }
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
     else if (ws_ok && a->a_mode == DP_A_CONV && !(dbg & 32) && tiles256 < num_cus() &&
-             (a->K >= 4608 || ((dbg & (1 << 27)) && a->K >= 2304 && tiles256 >= 128) ||
-              ((dbg & (1 << 28)) && a->K >= 2304 && tiles256 >= 32))) {
+             a->K >= 4608) {
       // Implicit convs with fewer 256 x 256 tiles than CUs and K >= 4608 (the decoder's
       // 512/1024-channel projections at 48^2 - 192^2) on the stream-K engine, each
       // tile's K range split (sk_grid): 153 -> 108, 152 -> 112, 152 -> 126 us in-frame
@@ -191,23 +189,26 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       else if (tile == DP_TILE_8PH_256x256 && (dbg & 16384)) tile = DP_TILE_BIG_256x256;
     }
   }
-  // split-K for small grids of long-K GEMMs (the decoder's 48^2 / 96^2 convs and projections,
-  // fuse_lowres): with <= a third as many 256 x 256 tiles as CUs, each tile's K steps go to
-  // S = min(CUs / tiles, K steps / 2, workspace slabs, 32) workgroups, then one reduce launch
-  // (DP_TILE_SPLITK_256x256; debug 1 << 27: off)
+  // split-K for small grids of long-K GEMMs (DP_TILE_SPLITK_256x256, an explicit hint; needs a
+  // workspace): each 256 x 256 tile's K steps go to S = min(CUs / tiles, K steps / 2, workspace
+  // slabs, 32) workgroups, then one reduce launch.  Not the auto choice: alone it takes the
+  // decoder's 48^2 / 96^2 convs and projections from 49 - 115 to 34 - 74 us, but in the frame
+  // their few-workgroup launches already share the chip with the decoder's other streams, and
+  // taking every CU made the frame slower (47.64 vs 48.05 fps; K >= 4608 only: 47.80; at most
+  // half the CUs: 48.04 -- profiles/r04o_splitk_ab/, r04n_splitk_ab/, r04m_splitk/)
   int ksplit = 1;
-  if (a->tile == DP_TILE_AUTO && ws_ok && !(dbg & (1 << 27)) && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
-      !a->row_group && !a->head_w && !a->head_corr && !lnp && !lnc) {
+  if (tile == DP_TILE_SPLITK_256x256) {
+    if (!ws_ok || a->N % 256 != 0 || a->store_mode != DP_STORE_ROWS || a->row_group || a->head_w || a->head_corr ||
+        lnp || lnc)
+      return DP_ERR_ARG;
     const long long ncu = num_cus(), kt = a->K / BK;
     const long long slab = (long long)a->M * a->N * 4;
-    long long sp = tiles256 > 0 ? ncu / tiles256 : 0;
+    long long sp = ncu / tiles256;
     if (sp > kt / 2) sp = kt / 2;
     if (sp > (a->workspace_bytes - SK_FLAG_BYTES) / slab) sp = (a->workspace_bytes - SK_FLAG_BYTES) / slab;
     if (sp > 32) sp = 32;
-    if (sp >= 3) {
-      tile = DP_TILE_SPLITK_256x256;
-      ksplit = (int)sp;
-    }
+    if (sp < 2) return DP_ERR_SHAPE;
+    ksplit = (int)sp;
   }
   // byte extent of C for the persistent engine's bounded buffer stores (0: not eligible)
   unsigned c_bytes = 0;

@@ -91,23 +91,25 @@ def test_gemm_plan_tile_choice():
     rc, tile, wgs = plan(20195, 3072, 1024, tile=_lib.DP_TILE_STREAMK_256x256, workspace=256, workspace_bytes=ws)
     assert rc == 0 and tile == _lib.DP_TILE_STREAMK_256x256 and 1 <= wgs <= 256
 
-    # decoder 3x3 convs: small grids (<= a third as many 256 x 256 tiles as CUs) of long-K GEMMs
-    # go to split-K + reduce (needs a workspace): split = min(CUs / tiles, K steps / 2, workspace
-    # slabs, 32); long-K projections with more tiles to stream-K; without a workspace the
-    # data-parallel engines
+    # decoder 3x3 convs: long-K projections with < 1 tile per CU go to stream-K with
+    # split K ranges (needs a workspace); K = 2304 small grids stay data-parallel
     def conv(S, cin, **kw):
         return plan(S * S, 256, 9 * cin, a_mode=_lib.DP_A_CONV, in_h=S, in_w=S, in_c=cin, k_h=3, k_w=3,
                     stride=1, pad=1, out_h=S, out_w=S, **kw)
     wsk = dict(workspace=256, workspace_bytes=ws)
-    assert conv(48, 1024, **wsk)[1:] == (_lib.DP_TILE_SPLITK_256x256, 9 * 28)     # 9 tiles x 28 (CUs / tiles)
-    assert conv(96, 1024, **wsk)[1:] == (_lib.DP_TILE_SPLITK_256x256, 36 * 7)     # 36 tiles x 7 (CUs / slabs)
-    assert conv(48, 256, **wsk)[1:] == (_lib.DP_TILE_SPLITK_256x256, 9 * 18)      # K = 2304: 36 steps / 2
-    assert conv(96, 256, **wsk)[1:] == (_lib.DP_TILE_SPLITK_256x256, 36 * 7)
+    assert conv(48, 1024, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 9 * 6)     # 9 tiles x split 6
+    assert conv(96, 1024, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 36 * 6)    # 36 tiles x split 6
     assert conv(192, 512, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 256)       # 144 tiles over 256 CUs
-    assert conv(48, 1024)[1] not in (_lib.DP_TILE_STREAMK_256x256, _lib.DP_TILE_SPLITK_256x256)  # no workspace
-    assert conv(48, 256)[1] == _lib.DP_TILE_BIG_256x128
-    # split-K is the planner's choice only (it sizes the split): as a hint it is refused
-    assert conv(48, 256, tile=_lib.DP_TILE_SPLITK_256x256, **wsk)[0] == 1000
+    assert conv(48, 1024)[1] != _lib.DP_TILE_STREAMK_256x256                        # no workspace
+    assert conv(48, 256, **wsk)[1] == _lib.DP_TILE_BIG_256x128                     # K = 2304
+    # split-K + reduce: an explicit hint (needs a workspace); split = min(CUs / tiles, K steps / 2,
+    # workspace slabs, 32)
+    SPK = _lib.DP_TILE_SPLITK_256x256
+    assert conv(48, 1024, tile=SPK, **wsk)[1:] == (SPK, 9 * 28)
+    assert conv(96, 1024, tile=SPK, **wsk)[1:] == (SPK, 36 * 7)                      # 7 slabs of 9.4 MB
+    assert conv(48, 256, tile=SPK, **wsk)[1:] == (SPK, 9 * 18)                       # 36 K steps / 2
+    assert conv(48, 256, tile=SPK)[0] == 1000                                        # no workspace
+    assert conv(768, 256, tile=SPK, **wsk)[0] == 1001                                # 2304 tiles: no split
     # the 768^2 ResidualBlock convs (2304 tiles of 256 pixels): the 3x3 patch-conv engine; 384^2 not
     assert conv(768, 256, **wsk)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
     assert conv(384, 256, **wsk)[1] != _lib.DP_TILE_CV3_256x256

@@ -520,7 +520,7 @@ SPLITK_CASES = [
 @pytest.mark.parametrize("case", SPLITK_CASES, ids=[c[0] for c in SPLITK_CASES])
 @pytest.mark.parametrize("dt", DTYPES)
 def test_gemm_split_k_matches_reference_and_data_parallel(cuda, dt, case):
-    """Split-K for small grids (DP_TILE_SPLITK_256x256, planner-chosen with a workspace): the 256 x
+    """Split-K for small grids (DP_TILE_SPLITK_256x256 hint, with a workspace): the 256 x
     256 engine over K ranges writing fp32 partials, then the reduce launch with the row epilogue.
     vs an fp32 reference, close to the data-parallel engine (only the fp32 summation order
     differs), and bit-identical run to run (partials summed in split order)."""
@@ -556,11 +556,12 @@ def test_gemm_split_k_matches_reference_and_data_parallel(cuda, dt, case):
         C1, C2, C3 = X.clone(), X.clone(), X.clone()
     else:
         C1, C2, C3 = (torch.empty(M, N, dtype=dt, device=cuda) for _ in range(3))
-    tile, wgs = ops.gemm(A, B, C1, plan_only=True, workspace=ws, **kw)
-    assert tile == DP_TILE_SPLITK_256x256 and wgs > (M + 255) // 256 * (N // 256), (tile, wgs)
-    ops.gemm(A, B, C1, workspace=ws, **kw)
+    SPK = DP_TILE_SPLITK_256x256
+    tile, wgs = ops.gemm(A, B, C1, plan_only=True, workspace=ws, tile=SPK, **kw)
+    assert tile == SPK and wgs > (M + 255) // 256 * (N // 256), (tile, wgs)
+    ops.gemm(A, B, C1, workspace=ws, tile=SPK, **kw)
     ops.gemm(A, B, C2, tile=DP_TILE_BIG_256x256, **kw)
-    ops.gemm(A, B, C3, workspace=ws, **kw)
+    ops.gemm(A, B, C3, workspace=ws, tile=SPK, **kw)
     torch.cuda.synchronize()
     close(C1, ref, torch.float32 if (mode == "acc" and dt == torch.float16) else dt, f"split-K {name}")
     d = (C1.float() - C2.float()).abs().max().item()
