@@ -13,7 +13,10 @@
 // as 128-B key rows with the 16-B chunk XOR-swizzled on the SOURCE address: K by
 // (row >> 1) & 7 (conflict-free ds_read_b128 of 16 rows), V by 64-B halves on odd
 // row pairs, read transposed with ds_read_b64_tr_b16 (conflict-free).  Q stays in
-// registers; 4 workgroups (16 waves) per CU.
+// registers; 3 workgroups (12 waves) per CU, 152 VGPRs: in the steady state both halves' S^T
+// MFMAs go first (K fragments read up front), so the second half's run on the matrix core while
+// the first half's softmax runs on the VALU (4 workgroups at 128 VGPRs left the compiler no room
+// to overlap them: 66.2 -> 64.2 us, profiles/r04q_attn_3wg/).
 // Softmax in log2 units: one FMA + exp2 per score against a running max that only the
 // first half key tile sets (an overflow, checked once at the end, sends the workgroup
 // through an exact per-tile-max pass), VALU row sums.
@@ -95,7 +98,7 @@ __device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, uint32
 #endif
 
 template <typename K_, bool PRE>
-__global__ void __launch_bounds__(256, 4)
+__global__ void __launch_bounds__(256, 3)
 attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int heads, int nq, float sl2, int dbg) {
   __shared__ __attribute__((aligned(1024))) char smem[2][2 * TILE_B];   // [stage][K tile | V tile]
   auto stage_of = [](int t) { return t & 1; };
@@ -196,25 +199,32 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
   // seq % 64 != 0): keys past seq are masked.  setmax: take this half tile's max (exact:
   // every half tile, with the deferred rescale; lazy: the first one, which sets m_run).
   // `exact` is a workgroup-uniform runtime flag, so the redo pass reuses this code.
-  auto do_half = [&](int t, int kb, auto partial_tag, bool setmax, bool exact) __attribute__((always_inline)) {
-    constexpr bool PARTIAL = decltype(partial_tag)::value;
-    const int cur = stage_of(t);
-    const int kbase = t * KT;
-    const char* K = smem[cur];
-    const char* V = smem[cur] + TILE_B;
-    // PRE, lazy max already set: the accumulator carries -m_run, P = 2^S directly
-    const bool off = PRE && !setmax && !exact;
+  // S^T of one 32-key half: 4 chained MFMAs (accumulator started at -m_run when `off`)
+  auto score = [&](int t, int kb, bool off) __attribute__((always_inline)) {
+    const char* K = smem[stage_of(t)];
     f32x16_t s;
+    uint4 kf[4];     // the half's K fragments read up front: one LDS latency, not four
+    #pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
     #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const uint4 kf = *(const uint4*)(K + k_off(kb * 32 + l32, 2 * ks + hi));
       f32x16_t c0 = f32x16_t{};
       if (off) {
         #pragma unroll
         for (int r = 0; r < 16; ++r) c0[r] = -m_run;
       }
-      s = K_::mfma32(kf, qf[ks], ks == 0 ? c0 : s);
+      s = K_::mfma32(kf[ks], qf[ks], ks == 0 ? c0 : s);
     }
+    return s;
+  };
+  // the rest of a half: mask, max, P = 2^S, row sums, O^T += V^T P^T
+  auto finish = [&](int t, int kb, f32x16_t s, auto partial_tag, bool setmax, bool exact)
+                    __attribute__((always_inline)) {
+    constexpr bool PARTIAL = decltype(partial_tag)::value;
+    const int cur = stage_of(t);
+    const int kbase = t * KT;
+    const char* V = smem[cur] + TILE_B;
+    const bool off = PRE && !setmax && !exact;
     if constexpr (PARTIAL) {
       #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -276,11 +286,23 @@ attn_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int seq, int hea
       }
     }
   };
+  auto do_half = [&](int t, int kb, auto partial_tag, bool setmax, bool exact) __attribute__((always_inline)) {
+    finish(t, kb, score(t, kb, PRE && !setmax && !exact), partial_tag, setmax, exact);
+  };
   // a 64-key tile = two halves; the second half of a partial tile is skipped when it holds no key
   auto do_tile = [&](int t, auto partial_tag, bool first, bool exact) __attribute__((always_inline)) {
     constexpr bool PARTIAL = decltype(partial_tag)::value;
     if (!active) return;
     const bool two = !PARTIAL || t * KT + 32 < seq;
+    if (!PARTIAL && PRE && !first && !exact) {
+      // steady state (running max fixed): both halves' S^T MFMAs first, so the second half's
+      // run on the matrix core while the first half's softmax runs on the VALU
+      const f32x16_t s0 = score(t, 0, true);
+      const f32x16_t s1 = score(t, 1, true);
+      finish(t, 0, s0, partial_tag, false, false);
+      finish(t, 1, s1, partial_tag, false, false);
+      return;
+    }
     do_half(t, 0, partial_tag, exact || first, exact);
     if (two) do_half(t, 1, partial_tag, exact, exact);
   };
