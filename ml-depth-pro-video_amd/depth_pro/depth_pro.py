@@ -113,8 +113,8 @@ class Transform:
         self.precision = precision
 
     def __call__(self, image) -> torch.Tensor:
-        if torch.is_tensor(image):          # a uint8 HxWx3 frame already on the device (frame loops)
-            src = image.to(self.device)
+        if torch.is_tensor(image):          # a uint8 HxWx3 frame on the device or in (pinned) host memory
+            src = image.to(self.device, non_blocking=True)
             if src.dtype != torch.uint8 or src.dim() != 3 or src.shape[2] != 3:
                 raise TypeError(f"transform expects an HxWx3 uint8 image, got {src.dtype} {tuple(src.shape)}")
             src = src.contiguous()

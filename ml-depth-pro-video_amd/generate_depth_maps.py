@@ -144,6 +144,11 @@ def _load(image_path: str, downscale_factor: float):
     image, _, f_px = depth_pro.load_rgb(image_path)
     if downscale_factor != 1.0 and downscale_factor > 0 and f_px is not None:
         f_px = f_px * downscale_factor
+    if torch.cuda.is_available():
+        # into pinned host memory here, in the decode thread: the upload is then an asynchronous
+        # copy on the frame's stream, so the main thread queues frame i+1 while frame i computes
+        # (a pageable upload blocks the host until the GPU has finished every earlier frame)
+        image = torch.from_numpy(np.ascontiguousarray(image)).pin_memory()
     return image, f_px
 
 
@@ -156,7 +161,8 @@ def _downscale(image: np.ndarray, downscale_factor: float, device: torch.device)
     from depth_pro import ops
 
     h, w = image.shape[:2]
-    src = torch.from_numpy(np.ascontiguousarray(image)).to(device, non_blocking=True)
+    src = image if torch.is_tensor(image) else torch.from_numpy(np.ascontiguousarray(image))
+    src = src.to(device, non_blocking=True)
     return ops.resize_u8_cv(src, int(h * downscale_factor), int(w * downscale_factor), area=downscale_factor < 1.0)
 
 
@@ -341,7 +347,7 @@ def _points(depth: torch.Tensor, f_px, image):
     and its copy into pinned host buffers, on the current stream, without a host synchronisation:
     full-size buffers + the point count (the writer slices them after the frame's event)."""
     h, w = depth.shape
-    rgb = image.to(depth.device) if torch.is_tensor(image) else \
+    rgb = image.to(depth.device, non_blocking=True) if torch.is_tensor(image) else \
         torch.from_numpy(np.ascontiguousarray(image)).to(depth.device, non_blocking=True)
     xyz, _, cols, count = PC.depth_to_points_async(depth, f_px, w, h, rgb=rgb)
     out = []

@@ -114,7 +114,7 @@ def main():
     t_enc = (time.time() - t) / len(hosts)
     t_ply = None
     if args.pointcloud:
-        img_dev = torch.from_numpy(imgs[0]).to(dev)
+        img_dev = (imgs[0] if torch.is_tensor(imgs[0]) else torch.from_numpy(imgs[0])).to(dev)
         f = m.infer(transform(imgs[0]))["focallength_px"]
         xyz, _, cols, count = PC.depth_to_points_async(depths[0], f, W, H, rgb=img_dev)
         torch.cuda.synchronize()
