@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="only the 35 x 577 bf16 case, no torch reference")
     ap.add_argument("--log2q", action="store_true", help="time dp_attention_log2q (what the engine runs)")
+    ap.add_argument("--seq", type=int, default=577, help="sequence length of the --quick case")
     ap.add_argument("--ablate", action="store_true",
                     help="35 x 577 with each stage dropped in turn (needs the ablation build: make attnexp, "
                          "DP_MI355X_LIB=.../libdp_mi355x_attnexp.so)")
@@ -49,7 +50,7 @@ def main():
             print(f"{lab:22s} {ms*1e3:7.1f}us {flop/ms/1e9:6.1f}TF", flush=True)
         lib.dp_attn_debug_flags(0)
         return
-    cases = ((35, 577),) if args.quick else ((35, 577), (1, 577), (8, 2048))
+    cases = ((35, args.seq),) if args.quick else ((35, 577), (1, 577), (8, 2048))
     for batch, seq in cases:
         for dt in ((torch.bfloat16,) if args.quick else (torch.bfloat16, torch.float16)):
             qkv = torch.randn(batch * seq, 3 * H * hd, device=dev).to(dt)
