@@ -42,6 +42,7 @@ SHAPES = [  # (name, M, N, K, kw)
     ("conv3x3 96^2 256->256", 96 * 96, 256, 2304, {"conv": 96}),
     ("conv3x3 48^2 256->256", 48 * 48, 256, 2304, {"conv": 48}),
     # ResidualBlock second conv: ReLU prologue + residual epilogue (f16, as the decoder runs it)
+    ("rb conv 384^2", 384 * 384, 256, 2304, {"conv": 384, "rb": True}),
     ("rb conv 192^2", 192 * 192, 256, 2304, {"conv": 192, "rb": True}),
     ("rb conv 96^2", 96 * 96, 256, 2304, {"conv": 96, "rb": True}),
     ("rb conv 48^2", 48 * 48, 256, 2304, {"conv": 48, "rb": True}),
