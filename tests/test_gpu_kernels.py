@@ -177,11 +177,13 @@ def test_head_conv_with_fused_1x1(cuda, dt):
 @pytest.mark.parametrize("batch,seq,spike", [(2, 577, None), (1, 100, None), (3, 64, None), (1, 1, None),
                                              (2, 66, None), (1, 2, None), (1, 67, None),
                                              (2, 577, "tail"), (1, 130, "tail"), (2, 577, "mid"),
-                                             (1, 100, "mid")])
+                                             (1, 100, "mid"), (1, 576, None), (1, 640, None), (1, 1024, None),
+                                             (1, 200, None), (1, 1024, "mid")])
 @pytest.mark.parametrize("log2q", [False, True])
 def test_attention(cuda, dt, batch, seq, spike, log2q):
-    """seq 577 / 66 / 2 / 130 end in 1-2 leftover keys (the VALU tail), 100 / 67 in a partial
-    MFMA tile.  spike "tail": the LAST key of every sequence is the scaled query of token 0, so
+    """seq 577 / 66 / 2 / 130 end in 1-2 leftover keys (the VALU tail), 100 / 67 / 200 in a partial
+    MFMA tile; 576 / 640 / 1024 are whole key tiles (the steady loop with both score halves issued
+    ahead, the scalar-base LDS-DMA of full tiles), 576 with a half-empty last query block.  spike "tail": the LAST key of every sequence is the scaled query of token 0, so
     that query's running max jumps inside the tail -- the rescale branch there is exercised;
     "mid": key 70 (second key tile) is 40x that query, far above the max the first half key
     tile set: P overflows and the workgroup redoes its keys on the exact-max path.
