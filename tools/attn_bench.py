@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--quick", action="store_true", help="only the 35 x 577 bf16 case, no torch reference")
     ap.add_argument("--log2q", action="store_true", help="time dp_attention_log2q (what the engine runs)")
     ap.add_argument("--seq", type=int, default=577, help="sequence length of the --quick case")
+    ap.add_argument("--batch", type=int, default=35, help="images of the --quick case")
     ap.add_argument("--ablate", action="store_true",
                     help="35 x 577 with each stage dropped in turn (needs the ablation build: make attnexp, "
                          "DP_MI355X_LIB=.../libdp_mi355x_attnexp.so)")
@@ -50,10 +51,13 @@ def main():
             print(f"{lab:22s} {ms*1e3:7.1f}us {flop/ms/1e9:6.1f}TF", flush=True)
         lib.dp_attn_debug_flags(0)
         return
-    cases = ((35, args.seq),) if args.quick else ((35, 577), (1, 577), (8, 2048))
+    cases = ((args.batch, args.seq),) if args.quick else ((35, 577), (1, 577), (8, 2048))
     for batch, seq in cases:
         for dt in ((torch.bfloat16,) if args.quick else (torch.bfloat16, torch.float16)):
-            qkv = torch.randn(batch * seq, 3 * H * hd, device=dev).to(dt)
+            qkv = torch.randn(batch * seq, 3 * H * hd, device=dev)
+            if args.log2q:   # the engine's qkv epilogue scales Q by hd^-0.5 * log2 e
+                qkv[:, :H * hd] *= hd ** -0.5 * 1.4426950408889634
+            qkv = qkv.to(dt)
             out = torch.empty(batch * seq, H * hd, dtype=dt, device=dev)
             flop = 4.0 * batch * H * seq * seq * hd
             ms = timeit(lambda: ops.attention(qkv, out, batch, seq, H, hd, log2q=args.log2q))
