@@ -528,7 +528,8 @@ extern "C" int dp_abi_version(void) { return DP_ABI_VERSION; }
 extern "C" int dp_layernorm_stats(const float* x, int64_t ldx, int32_t rows, int32_t cols, void* xb, int64_t ldxb,
                                   float* part, int32_t dtype, dp_stream_t stream) {
   if (!x || !xb || !part) return DP_ERR_ARG;
-  if (rows <= 0 || ldx % 4 || ldxb % 8) return DP_ERR_ALIGN;
+  if (rows <= 0) return DP_ERR_SHAPE;
+  if (ldx % 4 || ldxb % 8) return DP_ERR_ALIGN;
   dim3 grid((rows + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
 #define DP_LS(V_) do { \

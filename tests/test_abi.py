@@ -146,3 +146,38 @@ def test_gemm_plan_tile_choice():
         assert deconv(384, 256, 256, **wsk)[1] == _lib.DP_TILE_STREAMK_256x256
     finally:
         lib.dp_gemm_debug_flags(0)
+
+
+def test_empty_inputs_are_refused_before_launch():
+    """Zero-size inputs (no rows / images / pixels) return DP_ERR_SHAPE (DP_ERR_ARG for an empty
+    group list) from every entry point that takes a size, before any launch (no GPU here: a launch
+    would return a HIP error instead).  The reference's torch ops raise on these shapes too."""
+    lib = _lib.load()
+    P = 4096                      # a dummy non-null pointer: never dereferenced on the host
+    f32, f64 = ctypes.c_float, ctypes.c_double
+    a = _lib.GemmArgs()
+    a.M, a.N, a.K = 0, 64, 64
+    a.A = a.B = a.C = P
+    a.lda = a.ldb = a.ldc = 64
+    calls = {
+        "gemm M=0": lambda: lib.dp_gemm(ctypes.byref(a), None),
+        "attention batch=0": lambda: lib.dp_attention(P, P, 0, 577, 16, 64, f32(0.125), 0, None),
+        "attention seq=0": lambda: lib.dp_attention(P, P, 1, 0, 16, 64, f32(0.125), 0, None),
+        "attention_log2q heads=0": lambda: lib.dp_attention_log2q(P, P, 1, 577, 0, 64, 0, None),
+        "layernorm rows=0": lambda: lib.dp_layernorm(P, 1024, P, P, P, 1024, 0, 1024, f32(1e-6), 0, None),
+        "layernorm_stats rows=0": lambda: lib.dp_layernorm_stats(P, 1024, 0, 1024, P, 1024, P, 0, None),
+        "normalize_u8 H=0": lambda: lib.dp_normalize_u8(P, 0, 100, P, 0, None),
+        "resize_bilinear OH=0": lambda: lib.dp_resize_bilinear(P, 0, 3, 10, 10, P, 0, 10, None),
+        "resize H=0": lambda: lib.dp_resize(P, 0, 3, 0, 10, P, 10, 10, 0, None),
+        "vit_cls_rows n=0": lambda: lib.dp_vit_cls_rows(P, P, P, 0, None),
+        "infer_epilogue H=0": lambda: lib.dp_infer_epilogue(P, 1536, 1536, P, 0, f64(0), 0, 10, P, P, P, None),
+        "resize_u8_cv OH=0": lambda: lib.dp_resize_u8_cv(P, 10, 10, P, 0, 5, 3, None),
+        "depth_to_points H=0": lambda: lib.dp_depth_to_points(P, 0, 10, P, f64(1.0), 1, P, P, P, P, None),
+        "depth_to_image n=0": lambda: lib.dp_depth_to_image(P, 0, P, P, 256, 0, P, None),
+    }
+    for name, call in calls.items():
+        assert call() == 1001, name
+    a.M, a.N = 64, 0
+    assert lib.dp_gemm(ctypes.byref(a), None) == 1001
+    a.N = 64
+    assert lib.dp_gemm_grouped(ctypes.byref(a), 0, None) == 1000
