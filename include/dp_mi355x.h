@@ -160,7 +160,11 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
    DP_TILE_SPLITK_256x256 (ABI 11, a hint only, needs a workspace): split-K for small grids -- the
    256 x 256 tiles' K steps split over up to (CUs / tiles) workgroups that write fp32 partials into
    the workspace, then a reduce launch sums them in split order and runs the epilogue
-   (DP_STORE_ROWS, no row groups / head); DP_ERR_SHAPE when no split of >= 2 fits. */
+   (DP_STORE_ROWS, no row groups / head); DP_ERR_SHAPE when no split of >= 2 fits.
+   Sizes: the 8-phase 320 x 256 engine, the persistent engines (P8PH, PBIG) and the patch-conv
+   engine keep 32-bit element offsets from the A / B bases, so they serve M * lda and N * ldb
+   below 2^31 only; past that the planner takes the 64-bit-pointer engines and a hint for one
+   of those returns DP_ERR_ARG. */
 
 int dp_gemm(const dp_gemm_args* args, dp_stream_t stream);
 

@@ -225,9 +225,11 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     const long long ext = ((4LL * a->M - 1) * a->ldc + a->dc_cout) * 2;
     if (ext < 0xFFFFFF00LL) dcv_bytes = (unsigned)ext;
   }
-  // the persistent engine keeps 32-bit operand offsets
-  if (a->a_mode == DP_A_DENSE && (long long)a->M * a->lda >= (1LL << 31)) c_bytes = dcv_bytes = 0;
-  if ((long long)a->N * a->ldb >= (1LL << 31)) c_bytes = dcv_bytes = 0;
+  // the persistent engines and the 8-phase 320 x 256 one keep 32-bit operand offsets (element
+  // offsets from the A / B bases): beyond 2^31 elements only the 64-bit-pointer engines run
+  const bool off32 = (a->a_mode != DP_A_DENSE || (long long)a->M * a->lda < (1LL << 31)) &&
+                     (long long)a->N * a->ldb < (1LL << 31);
+  if (!off32) c_bytes = dcv_bytes = 0;
   if ((tile == DP_TILE_PBIG_320x256 || tile == DP_TILE_PBIG_256x256) && (!c_bytes || a->N % 256)) return DP_ERR_ARG;
   // Multi-round GEMMs on the 320 x 256 / 256 x 256 engines (the ViT qkv: 768 tiles, the
   // 768^2 decoder convs: 2304) run persistent: the next tile's first K step loads under
@@ -278,7 +280,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   if (tile == DP_TILE_8PH_320x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_BIG_320x256 && !(dbg & (1 << 15)))) {
     const bool plain = a->a_mode == DP_A_DENSE && !a->relu_a && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
                        !a->R1 && !a->R2 && !a->pos && !a->row_group && !a->head_w && !a->head_corr &&
-                       !(dbg & (1 << 20));
+                       !(dbg & (1 << 20)) && off32;
     const bool epi_ok = (!a->accumulate && a->c_dtype != DP_F32) ||
                         (a->accumulate && a->c_dtype == DP_F32 && a->act == DP_ACT_NONE);
     if (tile == DP_TILE_8PH_320x256 && !(plain && epi_ok)) return DP_ERR_ARG;
@@ -290,7 +292,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   if (a->tile == DP_TILE_AUTO && !(dbg & (1 << 16)) && a->a_mode == DP_A_CONV && a->k_h == 3 && a->k_w == 3 &&
       a->stride == 1 && a->pad == 1 && a->in_h == a->in_w && a->out_h == a->in_h && a->out_w == a->in_w &&
       a->in_w % 16 == 0 && a->in_c % 64 == 0 && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
-      !a->row_group && !a->head_w && !a->head_corr && (long long)a->M * a->in_c < (1LL << 31) &&
+      !a->row_group && !a->head_w && !a->head_corr && (long long)a->M * a->in_c < (1LL << 31) && off32 &&
       a->c_dtype != DP_F32 && !a->gamma && !a->pos && !a->accumulate && a->act != DP_ACT_GELU &&
       (long long)(a->M / 256) * (a->N / 256) >= 4LL * num_cus())   // many rounds (the 768^2 maps; 384^2: 201 vs 185 us)
     tile = DP_TILE_CV3_256x256;

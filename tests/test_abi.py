@@ -85,6 +85,16 @@ def test_gemm_plan_tile_choice():
     assert plan(20195, 1024, 1024, tile=_lib.DP_TILE_BIG_320x256)[1:] == (_lib.DP_TILE_BIG_320x256, 64 * 4)
     assert plan(577, 3072, 1024)[1:] == (_lib.DP_TILE_BIG_256x128, 3 * 24)       # side encoders
     assert plan(768 * 768, 128, 2304)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)     # head.0 conv (N = 128)
+    # past 2^31 elements of A (M * lda) or B (N * ldb): only the engines with 64-bit operand
+    # pointers (the 8-phase 320 x 256 and the persistent engines keep 32-bit element offsets)
+    big_m = (1 << 21) + 5                                   # 2097157 x 1024 >= 2^31
+    assert plan(big_m, 1024, 1024)[1:] == (_lib.DP_TILE_BIG_320x256, 6554 * 4)
+    off32 = {_lib.DP_TILE_8PH_320x256, _lib.DP_TILE_P8PH_256x256, _lib.DP_TILE_PBIG_320x256,
+             _lib.DP_TILE_PBIG_256x256}
+    assert plan(big_m, 4096, 1024)[1] not in off32
+    assert plan(big_m, 1024, 1024, tile=_lib.DP_TILE_8PH_320x256)[0] == 1000
+    assert plan(big_m, 4096, 1024, tile=_lib.DP_TILE_P8PH_256x256)[0] == 1000
+    assert plan(big_m - 8, 1024, 1024)[1] in off32                      # 2097149 x 1024 < 2^31
     # stream-K is opt-in and needs a workspace
     assert plan(20195, 3072, 1024, tile=_lib.DP_TILE_STREAMK_256x256)[0] == 1000
     ws = lib.dp_gemm_workspace_size()

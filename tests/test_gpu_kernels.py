@@ -48,6 +48,28 @@ def test_gemm_dense_bias(cuda, dt, M, N, K):
     close(C, ref, dt, "gemm")
 
 
+def test_gemm_past_32bit_element_offsets(cuda):
+    """M * lda >= 2^31 (a 4.3 GB A): the planner leaves the 32-bit-offset engines (8-phase 320 x 256,
+    persistent) for the 64-bit-pointer ones; the last rows (offsets past 2^31 elements) and the
+    first rows vs fp32 torch."""
+    M, N, K = (1 << 21) + 5, 1024, 1024
+    dt = torch.bfloat16
+    g = torch.Generator(device=cuda).manual_seed(11)
+    A = torch.empty(M, K, dtype=dt, device=cuda)
+    for r0 in range(0, M, 1 << 18):
+        A[r0:r0 + (1 << 18)] = torch.randn(min(1 << 18, M - r0), K, device=cuda, generator=g).to(dt)
+    B = (torch.randn(N, K, device=cuda, generator=g) * K ** -0.5).to(dt)
+    bias = torch.randn(N, device=cuda, generator=g)
+    C = torch.full((M, N), float("nan"), dtype=dt, device=cuda)
+    tile, _ = ops.gemm(A, B, C, M=M, N=N, K=K, bias=bias, plan_only=True)
+    assert tile == DP_TILE_BIG_320x256
+    ops.gemm(A, B, C, M=M, N=N, K=K, bias=bias)
+    for rows in (slice(0, 2048), slice(M - 4096, M)):
+        ref = A[rows].float() @ B.float().t() + bias
+        close(C[rows], ref, dt, f"gemm rows {rows.start}..{rows.stop}")
+    assert torch.isfinite(C[::4099].float()).all()
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 def test_gemm_gelu_and_residual_accumulate(cuda, dt):
     g = torch.Generator().manual_seed(3)
