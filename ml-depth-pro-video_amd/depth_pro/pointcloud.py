@@ -77,17 +77,18 @@ def write_ply(path: str, points: np.ndarray, colors: Optional[np.ndarray] = None
         if col.shape[0] != n:
             raise ValueError("points and colors differ in length")
         props += ["property uchar red", "property uchar green", "property uchar blue"]
-        rec = np.empty(n, dtype=[("p", "<f8", 3), ("c", "u1", 3)])
-        rec["p"], rec["c"] = pts, col
-        body = rec.tobytes()
+        body = np.empty(n, dtype=[("p", "<f8", 3), ("c", "u1", 3)])   # the 27-byte vertex records
+        body["p"], body["c"] = pts, col
     else:
-        body = pts.tobytes()
+        body = pts
     header = "\n".join(["ply", "format binary_little_endian 1.0", f"element vertex {n}", *props, "end_header"]) + "\n"
     if not path.endswith(".ply"):
         path = path + ".ply"
     with open(path, "wb") as f:
         f.write(header.encode("ascii"))
-        f.write(body)
+        # straight from the array's buffer: no bytes copy of the ~224 MB body (4K frame) made with
+        # the GIL held, which serialised the loop's writer threads
+        f.write(memoryview(body).cast("B"))
     return path
 
 

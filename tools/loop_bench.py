@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--workers", type=int, default=None,
                     help="decode and encode threads each (default: the loop's own defaults)")
     ap.add_argument("--dir", default=None, help="scratch directory (default: a temp dir, removed)")
+    ap.add_argument("--ply-copy", action="store_true",
+                    help="A/B: the round-4 PLY writer (body copied to bytes with the GIL held before the write)")
     args = ap.parse_args()
     W, H = (int(v) for v in args.size.split("x"))
 
@@ -48,6 +50,20 @@ def main():
     import depth_pro
     import generate_depth_maps as G
     from depth_pro import pointcloud as PC
+
+    if args.ply_copy:
+        def write_ply_copy(path, points, colors=None):
+            pts = np.ascontiguousarray(np.asarray(points, dtype="<f8").reshape(-1, 3))
+            rec = np.empty(pts.shape[0], dtype=[("p", "<f8", 3), ("c", "u1", 3)])
+            rec["p"], rec["c"] = pts, colors
+            hdr = ("ply\nformat binary_little_endian 1.0\nelement vertex %d\nproperty double x\nproperty double y\n"
+                   "property double z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n"
+                   % pts.shape[0])
+            with open(path, "wb") as f:
+                f.write(hdr.encode("ascii"))
+                f.write(rec.tobytes())
+            return path
+        PC.write_ply = write_ply_copy
 
     root = args.dir or tempfile.mkdtemp(prefix="loop_bench_")
     src, dst = os.path.join(root, "frames"), os.path.join(root, "out")
@@ -126,6 +142,7 @@ def main():
     out = {
         "what": "generate_depth_maps.batch_generate_depth_maps end to end, 1 GPU",
         "frames": args.frames, "size": [W, H], "pointcloud": args.pointcloud, "raw": args.raw,
+        "ply_writer": "bytes copy" if args.ply_copy else "zero-copy",
         "decode_workers": n_dec, "encode_workers": n_enc, "frames_ok": n_ok,
         "loop_fps": round(args.frames / t_loop, 2),
         "stage_fps": {"decode_png_pool": round(len(paths) / t_dec, 2),
