@@ -67,25 +67,55 @@ def depth_to_points_async(depth_in: torch.Tensor, focallength_px: Union[float, t
     return xyz, valid, cols, rows[height]
 
 
+PLY_RECORD = 27   # bytes per vertex: double x, y, z + uchar red, green, blue
+
+
+def ply_records_async(xyz: torch.Tensor, cols: torch.Tensor) -> torch.Tensor:
+    """The PLY vertex records of `depth_to_points_async`'s buffers, interleaved on the device
+    ((H*W, 27) uint8: the 24 bytes of x, y, z then r, g, b -- the layout `write_ply` writes), so
+    that the frame loop's writer only writes bytes.  Queued on the current stream, no sync."""
+    n = xyz.shape[0]
+    rec = torch.empty(n, PLY_RECORD, dtype=torch.uint8, device=xyz.device)
+    rec[:, :24].copy_(xyz.view(torch.uint8).view(n, 24))
+    rec[:, 24:].copy_(cols.view(n, 3))
+    return rec
+
+
+def _ply_header(n: int, colored: bool) -> bytes:
+    props = ["property double x", "property double y", "property double z"]
+    if colored:
+        props += ["property uchar red", "property uchar green", "property uchar blue"]
+    return ("\n".join(["ply", "format binary_little_endian 1.0", f"element vertex {n}", *props, "end_header"])
+            + "\n").encode("ascii")
+
+
+def write_ply_records(path: str, records: np.ndarray) -> str:
+    """`write_ply` for vertex records already in file layout ((n, 27) uint8, `ply_records_async`)."""
+    rec = np.ascontiguousarray(records, dtype=np.uint8).reshape(-1, PLY_RECORD)
+    if not path.endswith(".ply"):
+        path = path + ".ply"
+    with open(path, "wb") as f:
+        f.write(_ply_header(rec.shape[0], True))
+        f.write(memoryview(rec).cast("B"))
+    return path
+
+
 def write_ply(path: str, points: np.ndarray, colors: Optional[np.ndarray] = None) -> str:
     """Binary little-endian PLY: double x, y, z (+ uchar red, green, blue)."""
     pts = np.ascontiguousarray(np.asarray(points, dtype="<f8").reshape(-1, 3))
     n = pts.shape[0]
-    props = ["property double x", "property double y", "property double z"]
     if colors is not None:
         col = np.ascontiguousarray(np.asarray(colors, dtype=np.uint8).reshape(-1, 3))
         if col.shape[0] != n:
             raise ValueError("points and colors differ in length")
-        props += ["property uchar red", "property uchar green", "property uchar blue"]
         body = np.empty(n, dtype=[("p", "<f8", 3), ("c", "u1", 3)])   # the 27-byte vertex records
         body["p"], body["c"] = pts, col
     else:
         body = pts
-    header = "\n".join(["ply", "format binary_little_endian 1.0", f"element vertex {n}", *props, "end_header"]) + "\n"
     if not path.endswith(".ply"):
         path = path + ".ply"
     with open(path, "wb") as f:
-        f.write(header.encode("ascii"))
+        f.write(_ply_header(n, colors is not None))
         # straight from the array's buffer: no bytes copy of the ~224 MB body (4K frame) made with
         # the GIL held, which serialised the loop's writer threads
         f.write(memoryview(body).cast("B"))

@@ -62,11 +62,12 @@ def raw_depth_u16(depth_np: np.ndarray) -> np.ndarray:
     return ((depth_np - min_depth) / (max_depth - min_depth) * 65535).astype(np.uint16)
 
 
-def _png_bytes(arr: np.ndarray, level: int = 1) -> bytes:
-    """PNG file bytes of an 8-bit RGB (H, W, 3) or 16-bit greyscale (H, W) image: filter type 0
-    on every row and one zlib stream (level 1) -- the same pixels as any PNG writer (the
-    reference's cv2.imwrite included), ~3x faster than PIL's adaptive filtering, and zlib runs
-    without the GIL, so writer threads scale."""
+def _png_parts(arr: np.ndarray, level: int = 1) -> list:
+    """The PNG file of an 8-bit RGB (H, W, 3) or 16-bit greyscale (H, W) image as a list of byte
+    pieces: filter type 0 on every row and one zlib stream (level 1) -- the same pixels as any PNG
+    writer (the reference's cv2.imwrite included), ~3x faster than PIL's adaptive filtering.
+    zlib (compress, crc32) runs without the GIL and nothing here copies the image or the
+    compressed stream with the GIL held, so the loop's writer threads scale."""
     import struct
     import zlib
 
@@ -81,17 +82,24 @@ def _png_bytes(arr: np.ndarray, level: int = 1) -> bytes:
     raw[:, 0] = 0
     raw[:, 1:] = rows
 
-    def chunk(tag: bytes, data: bytes) -> bytes:
-        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+    def chunk(tag: bytes, data) -> list:
+        crc = zlib.crc32(data, zlib.crc32(tag)) & 0xFFFFFFFF
+        return [struct.pack(">I", len(data)), tag, data, struct.pack(">I", crc)]
 
     ihdr = struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)
-    return (b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", zlib.compress(raw.tobytes(), level)) +
-            chunk(b"IEND", b""))
+    idat = zlib.compress(memoryview(raw).cast("B"), level)
+    return [b"\x89PNG\r\n\x1a\n", *chunk(b"IHDR", ihdr), *chunk(b"IDAT", idat), *chunk(b"IEND", b"")]
+
+
+def _png_bytes(arr: np.ndarray, level: int = 1) -> bytes:
+    """PNG file bytes of an 8-bit RGB (H, W, 3) or 16-bit greyscale (H, W) image (`_png_parts`)."""
+    return b"".join(_png_parts(arr, level))
 
 
 def _write_png(path: str, arr: np.ndarray) -> None:
     with open(path, "wb") as f:
-        f.write(_png_bytes(np.ascontiguousarray(arr)))
+        for part in _png_parts(np.ascontiguousarray(arr)):
+            f.write(part)
 
 
 _MODEL = {}
@@ -323,7 +331,7 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                     if status is not None:
                         status.check()          # raises: this frame is dropped, nothing written
                     if pc is not None:
-                        PC.write_ply(os.path.join(output_dir, f"{base}_points.ply"), *_points_host(pc))
+                        PC.write_ply_records(os.path.join(output_dir, f"{base}_points.ply"), _points_host(pc))
                     if gpu_img:
                         _write_png(path, _host_image(host))
                         return path
@@ -343,15 +351,16 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
 
 
 def _points(depth: torch.Tensor, f_px, image):
-    """Queue the frame's point cloud on the GPU (depth_to_3d, img_to_normalized_pointcloud.py:819-856)
-    and its copy into pinned host buffers, on the current stream, without a host synchronisation:
-    full-size buffers + the point count (the writer slices them after the frame's event)."""
+    """Queue the frame's point cloud on the GPU (depth_to_3d, img_to_normalized_pointcloud.py:819-856),
+    interleaved into PLY vertex records there, and their copy into a pinned host buffer, on the
+    current stream, without a host synchronisation: the full-size record buffer + the point count
+    (the writer slices it after the frame's event and writes it as it is)."""
     h, w = depth.shape
     rgb = image.to(depth.device, non_blocking=True) if torch.is_tensor(image) else \
         torch.from_numpy(np.ascontiguousarray(image)).to(depth.device, non_blocking=True)
     xyz, _, cols, count = PC.depth_to_points_async(depth, f_px, w, h, rgb=rgb)
     out = []
-    for t in (xyz, cols, count):
+    for t in (PC.ply_records_async(xyz, cols), count):
         hbuf = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
         hbuf.copy_(t, non_blocking=True)
         out.append(hbuf)
@@ -359,10 +368,9 @@ def _points(depth: torch.Tensor, f_px, image):
 
 
 def _points_host(pc):
-    """Writer-thread side (after the frame's event): exactly the valid points."""
-    xyz, cols, n_host = pc
-    n = int(n_host)
-    return xyz[:n].numpy(), cols[:n].numpy()
+    """Writer-thread side (after the frame's event): exactly the valid points' records."""
+    rec, n_host = pc
+    return rec[:int(n_host)].numpy()
 
 
 def main():

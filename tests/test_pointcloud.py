@@ -71,6 +71,22 @@ def test_ply_round_trip(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("h,w", [(2160, 3840), (37, 300)])
+def test_ply_records_on_device_write_the_same_file(cuda, tmp_path, h, w):
+    """The frame loop's PLY path (vertex records interleaved on the GPU, written as they are) gives
+    the same file bytes as `write_ply` of the host points and colours."""
+    d = depth_frame(h, w, seed=7)
+    rgb = np.random.default_rng(4).integers(0, 256, (h, w, 3), dtype=np.uint8)
+    xyz, _, cols, count = PC.depth_to_points_async(torch.from_numpy(d).to(cuda), 987.25, w, h,
+                                                   rgb=torch.from_numpy(rgb).to(cuda))
+    rec = PC.ply_records_async(xyz, cols)
+    n = int(count)
+    a = PC.write_ply_records(str(tmp_path / "gpu"), rec[:n].cpu().numpy())
+    b = PC.write_ply(str(tmp_path / "host"), xyz[:n].cpu().numpy(), cols[:n].cpu().numpy())
+    assert open(a, "rb").read() == open(b, "rb").read()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("h,w", [(2160, 3840), (1536, 1536), (37, 300), (1, 1)])
 def test_depth_to_points_bit_exact(cuda, h, w):
     d = depth_frame(h, w, seed=h + w)

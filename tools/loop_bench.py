@@ -40,8 +40,12 @@ def main():
     ap.add_argument("--workers", type=int, default=None,
                     help="decode and encode threads each (default: the loop's own defaults)")
     ap.add_argument("--dir", default=None, help="scratch directory (default: a temp dir, removed)")
-    ap.add_argument("--ply-copy", action="store_true",
-                    help="A/B: the round-4 PLY writer (body copied to bytes with the GIL held before the write)")
+    ap.add_argument("--png-copy", action="store_true",
+                    help="A/B: the PNG writer that copied the filtered image and the compressed stream "
+                         "into new bytes objects (GIL held) before one write")
+    ap.add_argument("--ply-host", action="store_true",
+                    help="A/B: PLY vertex records interleaved by the writer thread on the host (numpy) "
+                         "instead of on the GPU")
     args = ap.parse_args()
     W, H = (int(v) for v in args.size.split("x"))
 
@@ -51,19 +55,47 @@ def main():
     import generate_depth_maps as G
     from depth_pro import pointcloud as PC
 
-    if args.ply_copy:
-        def write_ply_copy(path, points, colors=None):
-            pts = np.ascontiguousarray(np.asarray(points, dtype="<f8").reshape(-1, 3))
-            rec = np.empty(pts.shape[0], dtype=[("p", "<f8", 3), ("c", "u1", 3)])
-            rec["p"], rec["c"] = pts, colors
-            hdr = ("ply\nformat binary_little_endian 1.0\nelement vertex %d\nproperty double x\nproperty double y\n"
-                   "property double z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n"
-                   % pts.shape[0])
+    if args.png_copy:
+        def write_png_copy(path, arr):
+            import struct
+            import zlib
+            arr = np.ascontiguousarray(arr)
+            if arr.dtype == np.uint16:
+                depth, ctype, rows = 16, 0, arr.astype(">u2").view(np.uint8).reshape(arr.shape[0], -1)
+            else:
+                depth, ctype, rows = 8, 2, arr.reshape(arr.shape[0], -1)
+            raw = np.empty((arr.shape[0], rows.shape[1] + 1), np.uint8)
+            raw[:, 0] = 0
+            raw[:, 1:] = rows
+
+            def chunk(tag, data):
+                return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+            ihdr = struct.pack(">IIBBBBB", arr.shape[1], arr.shape[0], depth, ctype, 0, 0, 0)
             with open(path, "wb") as f:
-                f.write(hdr.encode("ascii"))
-                f.write(rec.tobytes())
-            return path
-        PC.write_ply = write_ply_copy
+                f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", ihdr) + chunk(b"IDAT", zlib.compress(raw.tobytes(), 1))
+                        + chunk(b"IEND", b""))
+        G._write_png = write_png_copy
+
+    if args.ply_host:
+        def points_host_interleave(depth, f_px, image):
+            h, w = depth.shape
+            rgb = image.to(depth.device, non_blocking=True) if torch.is_tensor(image) else \
+                torch.from_numpy(np.ascontiguousarray(image)).to(depth.device, non_blocking=True)
+            xyz, _, cols, count = PC.depth_to_points_async(depth, f_px, w, h, rgb=rgb)
+            out = []
+            for t in (xyz, cols, count):
+                hb = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                hb.copy_(t, non_blocking=True)
+                out.append(hb)
+            return tuple(out)
+
+        def records_on_host(pc):
+            xyz, cols, cnt = pc
+            n = int(cnt)
+            rec = np.empty(n, dtype=[("p", "<f8", 3), ("c", "u1", 3)])
+            rec["p"], rec["c"] = xyz[:n].numpy(), cols[:n].numpy()
+            return rec.view(np.uint8).reshape(n, PC.PLY_RECORD)
+        G._points, G._points_host = points_host_interleave, records_on_host
 
     root = args.dir or tempfile.mkdtemp(prefix="loop_bench_")
     src, dst = os.path.join(root, "frames"), os.path.join(root, "out")
@@ -136,13 +168,18 @@ def main():
         torch.cuda.synchronize()
         n = int(count)
         a, c = xyz[:n].cpu().numpy(), cols[:n].cpu().numpy()
+        rec = PC.ply_records_async(xyz, cols)[:n].cpu().numpy()
         t = time.time()
-        PC.write_ply(os.path.join(root, "one.ply"), a, c)
+        if args.ply_host:
+            PC.write_ply(os.path.join(root, "one.ply"), a, c)
+        else:
+            PC.write_ply_records(os.path.join(root, "one.ply"), rec)
         t_ply = time.time() - t
     out = {
         "what": "generate_depth_maps.batch_generate_depth_maps end to end, 1 GPU",
         "frames": args.frames, "size": [W, H], "pointcloud": args.pointcloud, "raw": args.raw,
-        "ply_writer": "bytes copy" if args.ply_copy else "zero-copy",
+        "ply_records": "host (numpy)" if args.ply_host else "GPU",
+        "png_writer": "bytes copies" if args.png_copy else "zero-copy parts",
         "decode_workers": n_dec, "encode_workers": n_enc, "frames_ok": n_ok,
         "loop_fps": round(args.frames / t_loop, 2),
         "stage_fps": {"decode_png_pool": round(len(paths) / t_dec, 2),
