@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--workers", type=int, default=None,
                     help="decode and encode threads each (default: the loop's own defaults)")
     ap.add_argument("--dir", default=None, help="scratch directory (default: a temp dir, removed)")
+    ap.add_argument("--switch-ms", type=float, default=None,
+                    help="A/B: sys.setswitchinterval for the run (the GIL hand-off to the submitting thread)")
     ap.add_argument("--png-copy", action="store_true",
                     help="A/B: the PNG writer that copied the filtered image and the compressed stream "
                          "into new bytes objects (GIL held) before one write")
@@ -96,6 +98,10 @@ def main():
             rec["p"], rec["c"] = xyz[:n].numpy(), cols[:n].numpy()
             return rec.view(np.uint8).reshape(n, PC.PLY_RECORD)
         G._points, G._points_host = points_host_interleave, records_on_host
+
+    if args.switch_ms is not None:
+        import sys
+        sys.setswitchinterval(args.switch_ms / 1000.0)
 
     root = args.dir or tempfile.mkdtemp(prefix="loop_bench_")
     src, dst = os.path.join(root, "frames"), os.path.join(root, "out")
@@ -180,6 +186,7 @@ def main():
         "frames": args.frames, "size": [W, H], "pointcloud": args.pointcloud, "raw": args.raw,
         "ply_records": "host (numpy)" if args.ply_host else "GPU",
         "png_writer": "bytes copies" if args.png_copy else "zero-copy parts",
+        "switch_ms": args.switch_ms,
         "decode_workers": n_dec, "encode_workers": n_enc, "frames_ok": n_ok,
         "loop_fps": round(args.frames / t_loop, 2),
         "stage_fps": {"decode_png_pool": round(len(paths) / t_dec, 2),
