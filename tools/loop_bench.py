@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--workers", type=int, default=None,
                     help="decode and encode threads each (default: the loop's own defaults)")
     ap.add_argument("--dir", default=None, help="scratch directory (default: a temp dir, removed)")
+    ap.add_argument("--trace", action="store_true",
+                    help="time where the loop's submitting thread spends the timed run (waits vs work)")
     ap.add_argument("--switch-ms", type=float, default=None,
                     help="A/B: sys.setswitchinterval for the run (the GIL hand-off to the submitting thread)")
     ap.add_argument("--png-copy", action="store_true",
@@ -134,10 +136,32 @@ def main():
         shutil.copy(os.path.join(src, f"output_{k:04d}.png"), warm)
     G.batch_generate_depth_maps(warm, os.path.join(root, "warm_out"), **kw)
     torch.cuda.synchronize()
+    main_t = {}
+    if args.trace:
+        import concurrent.futures as cf
+        import threading
+        main_id = threading.get_ident()
+        orig_result, orig_infer, orig_img = cf.Future.result, m.infer, G._image_async
+
+        def timed(key, fn):
+            def w(*a, **k):
+                if threading.get_ident() != main_id:
+                    return fn(*a, **k)
+                t0 = time.perf_counter()
+                try:
+                    return fn(*a, **k)
+                finally:
+                    main_t[key] = main_t.get(key, 0.0) + time.perf_counter() - t0
+            return w
+        cf.Future.result = timed("future_waits", orig_result)
+        m.infer = timed("infer_call", orig_infer)
+        G._image_async = timed("image_async", orig_img)
     t = time.time()
     n_ok = G.batch_generate_depth_maps(src, dst, **kw)
     torch.cuda.synchronize()
     t_loop = time.time() - t
+    if args.trace:
+        cf.Future.result, m.infer, G._image_async = orig_result, orig_infer, orig_img
 
     paths = sorted(os.path.join(src, f) for f in os.listdir(src))
     # stage: decode alone (the loop's decoder: depth_pro.load_rgb in a pool)
@@ -187,6 +211,7 @@ def main():
         "ply_records": "host (numpy)" if args.ply_host else "GPU",
         "png_writer": "bytes copies" if args.png_copy else "zero-copy parts",
         "switch_ms": args.switch_ms,
+        "main_thread_ms_per_frame": {k: round(1000 * v / args.frames, 2) for k, v in main_t.items()} or None,
         "decode_workers": n_dec, "encode_workers": n_enc, "frames_ok": n_ok,
         "loop_fps": round(args.frames / t_loop, 2),
         "stage_fps": {"decode_png_pool": round(len(paths) / t_dec, 2),
