@@ -56,7 +56,7 @@ for S in $STEPS; do
     loop)
       # the video loop as users run it (configs 3 and 5): PNG frames -> GPU -> PNG (+ PLY)
       timeout -k 10 400 python -u tools/loop_bench.py --frames 64 --size 1536x1536 > $OUT/loop_1536.log 2>&1
-      timeout -k 10 400 python -u tools/loop_bench.py --frames 8 --size 3840x2160 --pointcloud > $OUT/loop_4k_pc.log 2>&1 ;;
+      timeout -k 10 400 python -u tools/loop_bench.py --frames 64 --size 3840x2160 --pointcloud > $OUT/loop_4k_pc.log 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
   echo "step $S ok"
