@@ -70,6 +70,21 @@ def test_ply_round_trip(tmp_path):
     assert np.array_equal(p3, pts) and c3 is None
 
 
+def test_ply_records_layout(tmp_path):
+    """The record interleave (x, y, z as 24 little-endian bytes, then r, g, b) and its writer give
+    `write_ply`'s file bytes; the frame loop runs the same torch ops on the device (GPU test below)."""
+    g = np.random.default_rng(5)
+    pts = g.standard_normal((777, 3))
+    cols = g.integers(0, 256, (777, 3), dtype=np.uint8)
+    rec = PC.ply_records_async(torch.from_numpy(pts), torch.from_numpy(cols))
+    assert rec.shape == (777, PC.PLY_RECORD) and rec.dtype == torch.uint8
+    a = PC.write_ply_records(str(tmp_path / "r"), rec.numpy())
+    b = PC.write_ply(str(tmp_path / "w"), pts, cols)
+    assert open(a, "rb").read() == open(b, "rb").read()
+    p2, c2 = PC.read_ply(a)
+    assert np.array_equal(p2, pts) and np.array_equal(c2, cols)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("h,w", [(2160, 3840), (37, 300)])
 def test_ply_records_on_device_write_the_same_file(cuda, tmp_path, h, w):
