@@ -30,6 +30,15 @@ from .spec import DEPTH, EMBED_DIM, HEADS, IMG_SIZE, MLP_DIM, TOKENS
 # comma list of {side, attn, ln, vitgemm, decoder, head}.
 _ABLATE = set(filter(None, os.environ.get("DP_ABLATE", "").split(",")))
 
+
+def ln_fold_enabled() -> bool:
+    """Whether the patch encoder runs with its LayerNorms folded into qkv / fc1:
+    DP_LN_FOLD=1 (default), and no 'ln' / 'vitgemm' ablation -- those drop the standalone
+    LayerNorms / the ViT GEMMs, which only the unfolded path has as separate launches.
+    Read once at pack time: the packed set holds only the weights of the path chosen here."""
+    return os.environ.get("DP_LN_FOLD", "1") == "1" and not ({"ln", "vitgemm"} & _ABLATE)
+
+
 NWIN = 35
 TOK = TOKENS            # 577
 PTOK = TOKENS - 1       # 576
@@ -136,9 +145,13 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code) 
     vdt, dt = ops.torch_dtype(vcode), ops.torch_dtype(dcode)
     g = lambda k: sd[k].detach().to(device)  # noqa: E731
     P: Dict[str, object] = {}
+    fold = ln_fold_enabled()
     for vit in ("encoder.patch_encoder.", "encoder.image_encoder.", "fov.encoder.0."):
         if vit + "cls_token" not in sd:
             continue
+        # the patch encoder with its LayerNorms folded reads only the folded qkv / fc1 (below): the
+        # unfolded ones (350 MB of 16-bit weights) are not packed
+        folded = fold and vit == "encoder.patch_encoder."
         P[vit + "cls"] = _f32(g(vit + "cls_token")).reshape(D)
         P[vit + "pos"] = _f32(g(vit + "pos_embed")).reshape(TOK, D)
         P[vit + "pe.w"] = g(vit + "patch_embed.proj.weight").reshape(D, -1).to(vdt).contiguous()
@@ -149,10 +162,12 @@ def pack_weights(sd: Dict[str, torch.Tensor], device: torch.device, dtype_code) 
                       "attn.proj.bias", "mlp.fc1.bias", "mlp.fc2.bias", "ls1.gamma", "ls2.gamma"):
                 P[b + n] = _f32(g(b + n))
             for n in ("attn.qkv.weight", "attn.proj.weight", "mlp.fc1.weight", "mlp.fc2.weight"):
+                if folded and n in ("attn.qkv.weight", "mlp.fc1.weight"):
+                    continue
                 P[b + n] = g(b + n).to(vdt).contiguous()
         P[vit + "norm.weight"] = _f32(g(vit + "norm.weight"))
         P[vit + "norm.bias"] = _f32(g(vit + "norm.bias"))
-        if vit == "encoder.patch_encoder.":
+        if folded:
             # norm1 / norm2 folded into the qkv / fc1 that consume them (ops.fold_layernorm): the
             # patch encoder's residual GEMMs hand the next Linear 16-bit rows + chunk statistics
             # instead of a LayerNorm pass (Engine._vit); the qkv's log2q gamma rides
@@ -257,13 +272,17 @@ class FrameStatus:
     `check()` waits for that frame's copy only and raises DPError if the frame is bad, so a caller
     that checks before writing a frame's files drops exactly the bad frame (generate_depth_maps,
     depth-pro-run).  A status is reported once: after `check()` (or `Engine.check_status`) has
-    seen it, later `check_status` sweeps skip it."""
+    seen it, later `check_status` sweeps skip it.  A caller that takes a frame's status to check it
+    itself later (`claim()`, the frame loop's writer threads) OWNS it: the engine-wide sweep then
+    never reports that frame, so it is reported (and dropped) by its owner only -- not also by
+    whichever `infer` call happens to run after it finished."""
 
     def __init__(self, frame: int, words: torch.Tensor, event: torch.cuda.Event):
         self.frame = frame
         self.words = words            # pinned int32: [workspace error words..., non-finite count]
         self.event = event
         self.reported = False
+        self.owned = False            # claimed by a caller that checks it itself (claim)
 
     def ready(self) -> bool:
         return self.event.query()
@@ -285,6 +304,11 @@ class FrameStatus:
         if msg is not None:
             raise DPError(f"frame {self.frame}: {msg}")
 
+    def claim(self) -> "FrameStatus":
+        """Take ownership (see the class doc): the engine's sweep no longer reports this frame."""
+        self.owned = True
+        return self
+
 
 class BatchStatus:
     """The FrameStatus of every frame of one `DepthPro.infer` / `forward` call, as one status:
@@ -300,6 +324,15 @@ class BatchStatus:
 
     def ready(self) -> bool:
         return all(f.ready() for f in self.frames)
+
+    def claim(self) -> "BatchStatus":
+        """Take ownership of these frames' health: the caller promises to `check()` this status
+        itself (e.g. in a writer thread after the frame's event), so the engine's non-blocking
+        sweep at the next `infer` / `forward` never reports them (a bad frame is dropped once, by
+        its owner, and the next frame is not dropped in its place).  Returns self."""
+        for f in self.frames:
+            f.owned = True
+        return self
 
     def error(self) -> Optional[str]:
         bad = [(f.frame, e) for f in self.frames for e in [f.error()] if e is not None]
@@ -349,9 +382,12 @@ class Engine:
         S = IMG_SIZE
         self.x0 = e(3, S, S, dtype=torch.float32)           # network input (normalized, 1536^2)
         self.cols = e(NWIN * PTOK, 768, dtype=vdt)
-        # patch encoder LayerNorms folded into its GEMMs (pack_weights, _vit); DP_LN_FOLD=0: standalone
-        self.ln_fold = os.environ.get("DP_LN_FOLD", "1") == "1" and \
-            "encoder.patch_encoder.blocks.0.attn.qkv.fold.w" in packed
+        # patch encoder LayerNorms folded into its GEMMs (pack_weights, _vit): whichever path the packed
+        # set was made for (DP_LN_FOLD / ablations at pack time, ln_fold_enabled)
+        self.ln_fold = "encoder.patch_encoder.blocks.0.attn.qkv.fold.w" in packed
+        if self.ln_fold != ln_fold_enabled():
+            raise DPError("packed weights were made for the other LayerNorm path (DP_LN_FOLD / DP_ABLATE "
+                          "differ from when they were packed)")
         self.vp = _ViTBuffers(NWIN * TOK, vdt, dev, dt, ln_fold=self.ln_fold)     # patch encoder (35 windows)
         # image + FOV encoders, run as one grouped ViT (rows 0..576 image, 577..1153 FOV)
         self.side_vits = ["encoder.image_encoder."] + (["fov.encoder.0."] if self.use_fov else [])
@@ -804,7 +840,7 @@ class Engine:
     def _sweep(self, block: bool = False, block_oldest: bool = False) -> None:
         keep = []
         for j, st in enumerate(self._recent):
-            if st.reported:
+            if st.reported or st.owned:       # checked already, or its owner checks it (claim)
                 continue
             if block or st.ready() or (block_oldest and j == 0):
                 if st.error() is not None:
@@ -818,7 +854,7 @@ class Engine:
         done).  Each frame's status is reported once: checked frames leave the list, so a bad
         frame does not fail every later check."""
         self._sweep(block=block)
-        bad, self._unreported = [st for st in self._unreported if not st.reported], []
+        bad, self._unreported = [st for st in self._unreported if not (st.reported or st.owned)], []
         if bad:
             for st in bad:
                 st.reported = True

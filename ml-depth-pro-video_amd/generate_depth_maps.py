@@ -308,8 +308,12 @@ def batch_generate_depth_maps(input_dir, output_dir, pattern="*.png", downscale_
                     pred = model.infer(transform(image), f_px=f_px)
                     depth = pred["depth"]
                 # this frame's health (engine.FrameStatus: a timed-out stream-K hand-off, NaN / inf
-                # output), checked by the writer after the frame's event, before any file is written
+                # output), checked by the writer after the frame's event, before any file is written;
+                # claimed, so the next infer's sweep of finished frames leaves it to that writer (a
+                # bad frame is dropped once, by its writer, never the next frame in its place)
                 status = model.last_status() if hasattr(model, "last_status") else None
+                if status is not None and hasattr(status, "claim"):
+                    status.claim()
                 pc = None
                 gpu_img = False
                 if depth.is_cuda:

@@ -2,6 +2,7 @@
 and the pipelined directory loop on the GPU."""
 
 import os
+import time
 
 import numpy as np
 import pytest
@@ -84,3 +85,61 @@ def test_batch_loop_pointcloud_on_gpu(tmp_path, cuda):
     ref, valid = O.depth_to_3d(depth, float(pred["focallength_px"]), 480, 270)
     assert np.array_equal(pts, ref)
     assert np.array_equal(cols, img[valid])
+
+
+def test_bad_frame_dropped_once_by_its_writer(tmp_path):
+    """a bad frame whose status is already final when the NEXT frame is submitted (the
+    GPU finished it before its writer thread looked at it) is reported by its own writer only.
+    The loop claims each frame's status (BatchStatus.claim), so the next infer's non-blocking sweep
+    of finished frames (DepthPro._check_earlier -> Engine.check_status(block=False)) skips it:
+    frames 0 and 2 are written, frame 1 is dropped, and no frame is dropped in its place.  The
+    engine's sweep is the real one (Engine._sweep / check_status); the forward is a CPU stub whose
+    frames are finished at once."""
+    import threading
+
+    import torch
+    from PIL import Image
+
+    from depth_pro.engine import BatchStatus, Engine, FrameStatus
+
+    class Done:   # a frame event that has completed; its writer thread is slow to look at it
+        def __init__(self, delay):
+            self.delay = delay
+
+        def query(self):
+            return True
+
+        def synchronize(self):
+            if threading.current_thread() is not threading.main_thread():
+                time.sleep(self.delay)
+
+    class Model:
+        def __init__(self):
+            self.eng = Engine.__new__(Engine)
+            self.eng._recent, self.eng._unreported = [], []
+            self.n, self.last = 0, None
+
+        def infer(self, x, f_px=None):
+            self.eng.check_status(block=False)          # as DepthPro.infer before each call
+            words = torch.tensor([0, 7 if self.n == 1 else 0], dtype=torch.int32)
+            st = FrameStatus(self.n, words, Done(0.5 if self.n == 1 else 0.0))
+            self.eng._recent.append(st)
+            self.last = BatchStatus([st])
+            self.n += 1
+            return {"depth": torch.full(x.shape[:2], 2.0), "focallength_px": torch.tensor(1000.0)}
+
+        def last_status(self):
+            return self.last
+
+    src = tmp_path / "frames"
+    src.mkdir()
+    for k in range(3):
+        Image.fromarray(np.full((24, 32, 3), 40 * k, np.uint8)).save(src / f"output_{k:04d}.png")
+    model = Model()
+    n = G.batch_generate_depth_maps(str(src), str(tmp_path / "out"), pattern="output_*.png",
+                                    model=(model, lambda im: torch.as_tensor(np.asarray(im))), decode_workers=1,
+                                    encode_workers=1)
+    assert n == 2
+    assert sorted(os.listdir(tmp_path / "out")) == ["output_0000_depth.png", "output_0002_depth.png"]
+    assert model.n == 3
+    model.eng.check_status(block=True)                  # nothing owed: frame 1 was reported once
