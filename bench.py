@@ -188,6 +188,70 @@ def launch_ranks(n: int) -> None:
     sys.exit(subprocess.call(cmd))
 
 
+def timed_steps(infer_one, steps: int, warmup: int, world: int, dev: torch.device, sync=None,
+                on_gathered=None) -> dict:
+    """The measured loop of every rank (also driven over gloo by tests/test_bench_cli.py with a
+    stub model): `warmup` untimed steps, then exactly `steps` timed ones between a barrier +
+    device synchronisation on both sides; the elapsed time is the MAX over ranks (all_reduce).
+
+    Step n: `infer_one(n) -> (depth, status)` runs this rank's next frame (frame k -> rank
+    k mod world); for world > 1 its depth map is gathered to rank 0 asynchronously (RCCL's own
+    stream) while the next frame computes -- double-buffered: a depth tensor stays referenced until
+    its gather's wait(), which step n + 2 (or the drain) issues.  On rank 0,
+    `on_gathered(n, bufs)` sees step n's gathered maps (rank order) after that wait.
+    Returns {"elapsed": s (max over ranks), "statuses": [...], "frames_total": steps * world}."""
+    from depth_pro import distributed as D
+
+    sync = sync or torch.cuda.synchronize
+    pending = [None, None]
+    statuses = []          # status of every infer call of this rank (checked after the timed loop)
+    counter = [0]
+
+    def retire(j):
+        d, bufs, work, n = pending[j]
+        work.wait()
+        if on_gathered is not None and bufs is not None:
+            on_gathered(n, bufs)
+        pending[j] = None
+
+    def step(i):
+        if pending[i & 1] is not None:
+            retire(i & 1)
+        n = counter[0]
+        counter[0] += 1
+        d, st = infer_one(n)
+        statuses.append(st)
+        if world > 1:
+            bufs, work = D.gather_frames(d, dst=0, async_op=True)
+            pending[i & 1] = (d, bufs, work, n)
+
+    def drain(i0):
+        for j in (i0 & 1, (i0 + 1) & 1):     # oldest first: rank 0 sees the steps in order
+            if pending[j] is not None:
+                retire(j)
+
+    for i in range(warmup):
+        step(i)
+    drain(warmup)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    drain(steps)
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return {"elapsed": elapsed, "statuses": statuses, "frames_total": steps * world}
+
+
 # environment switches and their product defaults: a bench line is only printed for the defaults
 AB_KNOBS = {"DP_ABLATE": "0", "DP_GEMM_DEBUG": "0", "DP_ATTN_DEBUG": "0", "DP_SIDE_GATE": "0", "DP_LN_FOLD": "1"}
 
@@ -254,56 +318,17 @@ def main():
 
     # resident inputs: this rank's first `pool` frames of the stream (frame k -> rank k mod N), u8 in HBM
     frames = [torch.from_numpy(frame(k)).to(dev) for k in D.shard_frames(args.pool * world, rank, world)]
-    # frame i's depth map goes to rank 0 by an asynchronous RCCL gather (its own stream) while
-    # frame i+1 computes; the depth tensor stays referenced until that gather's work.wait()
-    pending = [None, None]
 
-    counter = [0]
-    statuses = []          # BatchStatus of every infer call this rank made (checked after the timed loop)
-
-    def step(i):
-        if pending[i & 1] is not None:
-            pending[i & 1][1].wait()
-            pending[i & 1] = None
-        n = counter[0]
-        counter[0] += 1
+    def infer_one(n):
         # the user's call: transform (u8 -> normalised fp32 on the GPU) + DepthPro.infer (copy into
         # the engine input, graph replay of the forward, depth / focal-length epilogue, status)
         with torch.no_grad():
             pred = model.infer(transform(frames[n % len(frames)]))
-        statuses.append(model.last_status())
-        if world > 1:
-            d = pred["depth"]
-            _, work = D.gather_frames(d, dst=0, async_op=True)
-            pending[i & 1] = (d, work)
+        return pred["depth"], model.last_status()
 
-    def drain():
-        for j in range(2):
-            if pending[j] is not None:
-                pending[j][1].wait()
-                pending[j] = None
-
-    for i in range(args.warmup):
-        step(i)
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-
-    frames_total = args.steps * world
+    run = timed_steps(infer_one, args.steps, args.warmup, world, dev)
+    elapsed, statuses = run["elapsed"], run["statuses"]
+    frames_total = run["frames_total"]
     fps = frames_total / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
     fps_per_gpu = fps / world
@@ -314,23 +339,36 @@ def main():
         refuse(f"rank {rank}: {len(bad)} of {len(statuses)} benched infer calls invalid "
                f"(first: {bad[0].error()})", 5)
 
-    # per-kernel roofline leg: one instrumented eager frame in the same stream layout as the
-    # captured graph (side encoders and decoder chains concurrent, so a launch sees the CUs the
-    # side kernels hold, as in the replayed frame and in a rocprofv3 kernel trace of it), HIP
-    # events on the launching stream around every launch; grouped by (kernel kind, shape)
-    groups = {}
+    # per-kernel leg (rank 0): instrumented eager frames with HIP events on the launching stream
+    # around every launch, grouped by (kernel kind, shape).  `groups`: a SERIAL frame (every launch on
+    # one stream, alone on the chip -- as in a rocprofv3 kernel trace, which serialises the graph's
+    # streams): its intervals are disjoint, so the per-kind table sums to the serial kernel time of a
+    # frame, and the dominant kernel's average is comparable with the committed rocprof summary.
+    # `groups_cc`: the product's concurrent stream layout (side encoders / decoder chains beside the
+    # main stream), where an interval also holds the time a launch waited for CUs other streams held:
+    # reported for the dominant kernel only, as its in-frame figure.
+    groups, groups_cc = {}, {}
+    serial_frame_ms = None
     if rank == 0:
         ops.normalize_u8(frames[0], eng.x0)
         for _ in range(2):
             eng.forward()                   # warm (no graph)
-        ops.profile_begin()
-        eng.forward()
-        rec = ops.profile_end()
-        for kind, flops, shape, kdt, ms in rec:
-            k = groups.setdefault((kind, shape, kdt), {"launches": 0, "ms": 0.0, "flop": 0.0})
-            k["launches"] += 1
-            k["ms"] += ms
-            k["flop"] += flops
+        for serial, grp in ((True, groups), (False, groups_cc)):
+            eng.serial_side = serial
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ops.profile_begin()
+            e0.record()
+            eng.forward()
+            e1.record()
+            rec = ops.profile_end()
+            if serial:
+                serial_frame_ms = e0.elapsed_time(e1)
+            for kind, flops, shape, kdt, ms in rec:
+                k = grp.setdefault((kind, shape, kdt), {"launches": 0, "ms": 0.0, "flop": 0.0})
+                k["launches"] += 1
+                k["ms"] += ms
+                k["flop"] += flops
+        eng.serial_side = False
 
     parity = None
     if rank == 0:
@@ -366,7 +404,11 @@ def main():
         dom_info = {"kind": dom_key[0], "shape": list(dom_key[1]), "dtype": str(dom_key[2]).replace("torch.", ""),
                     "launches_per_frame": dom["launches"],
                     "avg_us": round(dom_avg_us, 2), "flop_per_launch": dom_flop,
+                    "timing": "HIP events around each launch in a serial eager frame (alone on the chip)",
                     "share_of_frame_kernel_time": round(dom["ms"] / sum(g["ms"] for g in groups.values()), 3)}
+        cc = groups_cc.get(dom_key)
+        if cc:
+            dom_info["in_frame_concurrent_avg_us"] = round(1000.0 * cc["ms"] / cc["launches"], 2)
         traffic = None
         if dom_key[0].startswith("gemm"):
             M, N, K = dom_key[1]
@@ -413,8 +455,13 @@ def main():
                          "dominant_kernel": dom_info,
                          "frame": {"achieved": round(achieved, 1), "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                                    "basis": "fps_per_gpu x 19.247 TFLOP/frame (SURVEY 8d)"}},
+            # per-kind launch times of one SERIAL eager frame (disjoint intervals: they sum to
+            # serial_frame_kernel_ms; the graph-replayed step overlaps streams, so it is shorter)
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in kern.items()},
+            "kernels_basis": {"frame": "serial eager (every launch on one stream)",
+                              "serial_frame_ms": round(serial_frame_ms, 3),
+                              "serial_frame_kernel_ms": round(sum(k["ms"] for k in kern.values()), 3)},
             "parity": parity,
             "setup_s": round(t_setup, 1),
         }

@@ -208,10 +208,13 @@ def test_config4_collectives_over_rccl(tmp_path):
     assert res == {"equal": True, "gather_equal": True, "allreduce": 1.25}, res
 
 
-def test_frame_loop_drops_exactly_the_failed_frame(tmp_path, cuda):
+@pytest.mark.parametrize("sync_after", [False, True])
+def test_frame_loop_drops_exactly_the_failed_frame(tmp_path, cuda, sync_after):
     """Fault injection on frame 1 of 3 (a stream-K hand-off that gives up at once): the loop
     reports frame 1, writes nothing for it, and writes frames 0 and 2 (whose own forwards were
-    healthy: the failed forward's workspace check cleared the error word and the flags)."""
+    healthy: the failed forward's workspace check cleared the error word and the flags).
+    sync_after: the GPU has finished frame 1 before frame 2 is submitted, so frame 2's infer finds
+    frame 1's bad status final -- the loop's claim leaves it to frame 1's writer."""
     from PIL import Image
 
     import depth_pro
@@ -236,6 +239,8 @@ def test_frame_loop_drops_exactly_the_failed_frame(tmp_path, cuda):
                 return self.m.infer(x, f_px=f_px)
             finally:
                 lib.dp_gemm_debug_flags(0)
+                if sync_after and self.n == 1:
+                    torch.cuda.synchronize()
                 self.n += 1
 
         def last_status(self):
