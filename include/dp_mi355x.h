@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 11
+#define DP_ABI_VERSION 12
 int dp_abi_version(void);
 
 /*
@@ -132,12 +132,20 @@ typedef struct dp_gemm_args {
    *    (the 16-bit values, summed exactly); the epilogue's value before act is
    *      v = rstd * acc - rstd * mean * ln_colsum[n] + bias[n]
    *    with (mean, rstd) of the row merged from its K/128 chunks: LN(x) . W^T + b exactly, up
-   *    to where the 16-bit rounding falls (x instead of LN(x)). */
+   *    to where the 16-bit rounding falls (x instead of LN(x)).
+   *  producer on a SPLIT residual (ABI 12, ln_xl != NULL): the residual stream is held as two
+   *    16-bit arrays (dtype, [M][ldc]), x = ln_xb_out + ln_xl, read and updated in place:
+   *    x' = v + x;  ln_xb_out = x' rounded to 16 bits;  ln_xl = (x' - ln_xb_out) rounded to 16 bits
+   *    (~17 significant bits: the fp32 stream's error unchanged, tools/hilo_emul.py); ln_part_out
+   *    as above or NULL; C (fp32, [M][ldc]) is not read: NULL, or written with x' (for a reader of
+   *    the fp32 rows); accumulate = 1, act none, N % 128 == 0, M * ldc * 4 < 2^32 - 256.  8 instead
+   *    of 10 bytes of HBM traffic per element in a residual GEMM's epilogue. */
   float* ln_part_out;
   void* ln_xb_out;
   const float* ln_part_in;
   const float* ln_colsum;
   float ln_eps;
+  void* ln_xl;
 } dp_gemm_args;
 
 enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32 = 3,
@@ -223,10 +231,11 @@ int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, vo
  * fp32 x [rows][cols] (cols % 128 == 0, <= 2048) write x in 16 bits (xb [rows][ldxb], dtype) and
  * part fp32 [rows][cols/128][2] = (mean, M2) of each 128-column chunk -- what the residual GEMMs'
  * producer epilogue writes, for the rows no GEMM produced (the patch embed + cls rows that enter
- * ViT block 0).
+ * ViT block 0).  xl (ABI 12; NULL: none): the low part of the split residual, (x - xb) in 16 bits
+ * ([rows][ldxb]), so that xb + xl is the stream a split-residual producer (dp_gemm_args.ln_xl) reads.
  */
 int dp_layernorm_stats(const float* x, int64_t ldx, int32_t rows, int32_t cols, void* xb, int64_t ldxb,
-                       float* part, int32_t dtype, dp_stream_t stream);
+                       void* xl, float* part, int32_t dtype, dp_stream_t stream);
 
 /*
  * dp_layernorm_grouped: dp_layernorm over groups * rows_per_group rows, rows of group g taking

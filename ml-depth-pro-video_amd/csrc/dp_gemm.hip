@@ -76,7 +76,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   if (a->M <= 0 || a->N <= 0 || a->K <= 0) return DP_ERR_SHAPE;
   if (a->K % BK != 0 || a->N % 4 != 0) return DP_ERR_SHAPE;
   if (a->ldb % 8 != 0 || (a->a_mode == DP_A_DENSE && a->lda % 8 != 0)) return DP_ERR_ALIGN;
-  if (!a->A || !a->B || !a->C) return DP_ERR_ARG;
+  if (!a->A || !a->B || (!a->C && !a->ln_xl)) return DP_ERR_ARG;   // split-residual producer: C optional
   if (a->dtype != DP_BF16 && a->dtype != DP_F16) return DP_ERR_DTYPE;
   if (a->c_dtype != DP_BF16 && a->c_dtype != DP_F16 && a->c_dtype != DP_F32) return DP_ERR_DTYPE;
   if (a->c_dtype != DP_F32 && a->c_dtype != a->dtype) return DP_ERR_DTYPE;
@@ -109,10 +109,15 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // folded LayerNorm (ln_*): the 8-phase 320 x 256 engine only, producer = the fp32 residual
   // accumulate without activation (N % 128 == 0), consumer = 16-bit C over K = 1024 rows whose
   // gamma is folded into B / bias
-  const bool lnp = a->ln_part_out || a->ln_xb_out, lnc = a->ln_part_in || a->ln_colsum;
+  const bool lnp = a->ln_part_out || a->ln_xb_out || a->ln_xl, lnc = a->ln_part_in || a->ln_colsum;
   if (lnp && lnc) return DP_ERR_ARG;
-  if (lnp && (!a->ln_part_out || !a->ln_xb_out || !a->accumulate || a->c_dtype != DP_F32 || a->act != DP_ACT_NONE ||
-              a->N % 128 != 0))
+  if (lnp && !a->ln_xl && (!a->ln_part_out || !a->ln_xb_out || !a->accumulate || !a->C || a->c_dtype != DP_F32 ||
+                           a->act != DP_ACT_NONE || a->N % 128 != 0))
+    return DP_ERR_ARG;
+  // the split residual (ABI 12): x = ln_xb_out + ln_xl, both 16-bit [M][ldc], updated in place; part and
+  // an fp32 copy in C optional; every byte extent below the buffer-store bound
+  if (a->ln_xl && (!a->ln_xb_out || !a->accumulate || a->c_dtype != DP_F32 || a->act != DP_ACT_NONE ||
+                   a->N % 128 != 0 || a->ldc % 8 != 0 || (long long)a->M * a->ldc * 4 >= 0xFFFFFF00LL))
     return DP_ERR_ARG;
   if (lnc && (!a->ln_part_in || !a->ln_colsum || a->K != 1024 || a->accumulate || a->c_dtype == DP_F32 ||
               a->gamma || (a->act != DP_ACT_NONE && a->act != DP_ACT_GELU) || !(a->ln_eps > 0.f)))
@@ -314,7 +319,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.store_mode = a->store_mode; p.dc_h = a->dc_h; p.dc_w = a->dc_w; p.dc_cout = a->dc_cout;
   p.row_group = a->row_group; p.row_group_out = a->row_group_out; p.row_off = a->row_off;
   p.head_w = a->head_w; p.head_b = a->head_b; p.head_corr = a->head_corr;
-  p.ln_part_out = a->ln_part_out; p.ln_xb_out = (u16*)a->ln_xb_out;
+  p.ln_part_out = a->ln_part_out; p.ln_xb_out = (u16*)a->ln_xb_out; p.ln_xl = (u16*)a->ln_xl;
   p.ln_part_in = a->ln_part_in; p.ln_colsum = a->ln_colsum; p.ln_eps = a->ln_eps;
   p.ln_rs = nullptr;
   p.tiles_n = 1;
@@ -404,7 +409,7 @@ extern "C" int dp_gemm_grouped(const dp_gemm_args* a, int32_t groups, dp_stream_
         !y.R2 != !x.R2 || y.ldr2 != x.ldr2 || y.ldc != x.ldc || y.c_dtype != x.c_dtype ||
         y.accumulate != x.accumulate || y.store_mode != DP_STORE_ROWS || x.store_mode != DP_STORE_ROWS ||
         y.row_group != x.row_group || y.row_group_out != x.row_group_out || y.row_off != x.row_off ||
-        y.head_w || y.head_corr || y.N % 8 != 0 || y.ln_part_out || y.ln_xb_out || y.ln_part_in ||
+        y.head_w || y.head_corr || y.N % 8 != 0 || y.ln_part_out || y.ln_xb_out || y.ln_xl || y.ln_part_in ||
         y.ln_colsum)
       return DP_ERR_ARG;
     if (g == 0) p = q;

@@ -35,6 +35,7 @@ namespace dpg {
 
 constexpr int BK = 64;
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 constexpr int DP_MAX_GROUPS = 4;   // dp_gemm_grouped
 
@@ -73,6 +74,7 @@ struct GemmP {
   // LayerNorm folded across the GEMM boundary (dp_gemm_args.ln_*; the 8-phase 320 x 256 engine)
   float* ln_part_out;      // producer: (mean, M2) per 128-column chunk of the new C rows
   u16* ln_xb_out;          // producer: the new C rows in 16 bits ([M][ldc])
+  u16* ln_xl;              // producer on a split residual (hi = ln_xb_out, lo = ln_xl; read + written)
   const float* ln_part_in; // consumer: the A rows' chunk statistics ([M][K/128][2])
   const float* ln_colsum;  // consumer: sum_k B[n][k]
   float ln_eps;
@@ -1029,6 +1031,140 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
       : "v"(src), "s"(lds_dst)
       : "memory");
 }
+
+// Folded-LN producer on a SPLIT residual stream (dp_gemm_args.ln_xl, LNM = 3 of the 8-phase
+// 320 x 256 engine): the ViT residual x is held as two 16-bit arrays, x = hi + lo, hi =
+// ln_xb_out (the next GEMM's A operand anyway) and lo = ln_xl (what hi's rounding dropped, itself
+// rounded to 16 bits: about 17 significant bits against fp32's 24 -- the patch encoder's rel-L1
+// vs the fp32 reference 2.3789e-3 against 2.3788e-3 with an fp32 stream, bf16 hi alone 1.06e-2,
+// tools/hilo_emul.py).  Per element: x' = (acc + b) * gamma + (hi + lo) (the fp32 epilogue's
+// operation order), hi' = r16(x'), lo' = r16(x' - hi'); (mean, M2) of each row's 128 columns as
+// epilogue_acc32_wide_ln (when ln_part_out); C (fp32) = x' when given (never read).  8 B of HBM
+// per element instead of 10 (fp32 read + write, 16-bit hi write): the epilogue of a one-round
+// launch (proj / fc2) is HBM-bound.
+// Per 16-row fragment row fm: the wave's hi and lo rows (16 x 128 x 16 bit each) arrive by
+// LDS-DMA one fragment row ahead into a 2-deep per-wave staging ring (16-B chunks XOR-swizzled by
+// row on the source address: the MFMA-layout reads are conflict-free), are read in the MFMA
+// layout, updated in place, read back as rows and leave as 256-B row segments.  Every store is a
+// buffer store whose masked lanes (rows past M, an absent output) carry an out-of-range offset, so
+// each iteration issues a fixed number of VMEM instructions (ST below) and the counted wait for a
+// fragment row's DMA is a compile-time constant.  `slab`: the wave's LDS region, >= 17 KiB.
+template <typename K_, int FM, int FN>
+__device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[FM][FN], char* slab, int lane,
+                                                 int m_base, int n_base) {
+  #pragma clang fp contract(off)
+  static_assert(FN == 8, "128 columns per wave");
+  constexpr int ST = 8 + 1 + 8;       // VMEM stores per fragment row: C (8 x 16 B), part, hi + lo rows (8)
+  const int t = lane & 15, g = lane >> 4;
+  {
+    const int c = 4 * (lane & 31), n = n_base + c;
+    f32x4_t v;
+    if (lane < 32) v = (p.bias && n < p.N) ? *(const f32x4_t*)(p.bias + n) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    else v = (p.gamma && n < p.N) ? *(const f32x4_t*)(p.gamma + n) : f32x4_t{1.f, 1.f, 1.f, 1.f};
+    *(f32x4_t*)(slab + (lane < 32 ? 0 : 512) + c * 4) = v;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the constants, before any DMA is counted
+  const u16* const hi_in = p.ln_xb_out;
+  const u16* const lo_in = p.ln_xl;
+  constexpr unsigned OOB = 0xFFFFFFF0u;   // a masked store's offset: past every extent (host: < 0xFFFFFF00)
+  const unsigned row_b = (unsigned)(p.M * p.ldc * 2);              // bytes of hi / lo
+  const __amdgpu_buffer_rsrc_t rs_hi = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_xb_out, (short)0, (int)row_b, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_lo = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_xl, (short)0, (int)row_b, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_c = __builtin_amdgcn_make_buffer_rsrc(p.C ? p.C : (void*)p.ln_xl, (short)0,
+                                                                        p.C ? (int)(2 * row_b) : 0, 0x00020000);
+  const int nch = p.N / 128;
+  const __amdgpu_buffer_rsrc_t rs_pt = __builtin_amdgcn_make_buffer_rsrc(
+      p.ln_part_out ? (void*)p.ln_part_out : (void*)p.ln_xl, (short)0, p.ln_part_out ? (int)(p.M * nch * 8) : 0,
+      0x00020000);
+  const uint32_t slab_lds = __builtin_amdgcn_readfirstlane(lds_addr(slab)) + 1024;
+  // DMA of fragment row fm's hi / lo rows into staging buffer b: piece pc of an array = rows
+  // pc * 4 + lane / 16, 16 lanes x 16 B per 256-B row, logical chunk (lane & 15) ^ row
+  auto dma = [&](int fm, int b) __attribute__((always_inline)) {
+    #pragma unroll
+    for (int pc = 0; pc < 4; ++pc) {
+      const int r = pc * 4 + (lane >> 4);
+      const int m = min(m_base + fm * 16 + r, p.M - 1);
+      const long long o = (long long)m * p.ldc + n_base + (((lane & 15) ^ r) << 3);
+      glds16(hi_in + o, slab_lds + b * 8192 + pc * 1024);
+      glds16(lo_in + o, slab_lds + b * 8192 + 4096 + pc * 1024);
+    }
+  };
+  dma(0, 0);
+  #pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    char* const buf = slab + 1024 + (fm & 1) * 8192;
+    if (fm + 1 < FM) dma(fm + 1, (fm + 1) & 1);
+    // fragment row fm's DMA landed: younger are the previous row's ST stores and the next DMA
+    if (fm == 0) { if (FM > 1) wait_vmcnt<8>(); else wait_vmcnt<0>(); }
+    else if (fm + 1 < FM) wait_vmcnt<ST + 8>();
+    else wait_vmcnt<ST>();
+    const int m = m_base + fm * 16 + t;
+    const bool mok = m < p.M;
+    float sh = 0.f, s1 = 0.f, s2 = 0.f;
+    #pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int off = t * 256 + (((fn * 2 + (g >> 1)) ^ t) << 4) + (g & 1) * 8;
+      const uint2 h = *(const uint2*)(buf + off);
+      const uint2 l = *(const uint2*)(buf + 4096 + off);
+      const float xin[4] = {K_::to_f(h.x & 0xffff) + K_::to_f(l.x & 0xffff), K_::to_f(h.x >> 16) + K_::to_f(l.x >> 16),
+                            K_::to_f(h.y & 0xffff) + K_::to_f(l.y & 0xffff), K_::to_f(h.y >> 16) + K_::to_f(l.y >> 16)};
+      const f32x4_t b = *(const f32x4_t*)(slab + (fn * 16 + 4 * g) * 4);
+      const f32x4_t q = *(const f32x4_t*)(slab + 512 + (fn * 16 + 4 * g) * 4);
+      f32x4_t x;
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[fm][fn][r] + b[r];
+        x[r] = v * q[r] + xin[r];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, x), rs_c,
+                                             mok ? (unsigned)(((long long)m * p.ldc + n_base + fn * 16 + 4 * g) * 4)
+                                                 : OOB, 0, 0);
+      if (fn == 0) {
+        sh = __shfl(x[0], t);             // the row's value at column n_base (lane t, g = 0)
+        s1 = 0.f;
+        s2 = 0.f;
+      }
+      #pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = x[r] - sh;
+        s1 += d;
+        s2 += d * d;
+      }
+      uint2 wh, wl;
+      wh.x = K_::pack2(x[0], x[1]);
+      wh.y = K_::pack2(x[2], x[3]);
+      wl.x = K_::pack2(x[0] - K_::to_f(wh.x & 0xffff), x[1] - K_::to_f(wh.x >> 16));
+      wl.y = K_::pack2(x[2] - K_::to_f(wh.y & 0xffff), x[3] - K_::to_f(wh.y >> 16));
+      *(uint2*)(buf + off) = wh;
+      *(uint2*)(buf + 4096 + off) = wl;
+    }
+    // the row's 128 columns: 4 lanes (g) of 32 values each
+    s1 += __shfl_xor(s1, 16);
+    s2 += __shfl_xor(s2, 16);
+    s1 += __shfl_xor(s1, 32);
+    s2 += __shfl_xor(s2, 32);
+    {
+      const float mc = sh + s1 * (1.f / 128);
+      const float m2 = s2 - s1 * (s1 * (1.f / 128));
+      const unsigned po = (g == 0 && mok) ? (unsigned)(((long long)m * nch + n_base / 128) * 8) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(mc), __float_as_uint(m2)}, rs_pt, po, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's staging writes
+    #pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = k * 4 + (lane >> 4), chunk = lane & 15;
+      const int o = row * 256 + ((chunk ^ row) << 4);
+      const uint4 dh = *(const uint4*)(buf + o);
+      const uint4 dl = *(const uint4*)(buf + 4096 + o);
+      const int mm = m_base + fm * 16 + row;
+      const unsigned bo = mm < p.M ? (unsigned)(((long long)mm * p.ldc + n_base + chunk * 8) * 2) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{dh.x, dh.y, dh.z, dh.w}, rs_hi, bo, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{dl.x, dl.y, dl.z, dl.w}, rs_lo, bo, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read back before this buffer's next DMA
+  }
+}
+
 
 // LDS image of one operand tile: rows of BKT 16-bit elements (64 or 128 B), the
 // 16-B chunk index XOR-swizzled so that the 16 rows one ds_read_b128 lane group
@@ -2203,7 +2339,7 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
 // s+1 in phase 3 -- so each piece has 4+ phases to land and the count is 8 in steady state.
 // Dense A only; epilogues: the load-free MFMA-layout one (EACT = DP_ACT_*; 16-bit C) or the
 // fp32 residual-accumulate one (EACT = EPI_ACC + act).
-template <typename K_, int EACT, int LNM = 0>   // LNM: 1 folded-LN producer, 2 consumer
+template <typename K_, int EACT, int LNM = 0>   // LNM: 1 folded-LN producer, 2 consumer, 3 producer on hi + lo
 __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   constexpr int BM = 320;
   constexpr int A_BYTES = BM * 128, B_BYTES = 256 * 128, BUF = A_BYTES + B_BYTES;
@@ -2329,7 +2465,9 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
     return;
   }
   lds_barrier();   // the ring is free once every wave has left the K loop
-  if constexpr (LNM == 1)
+  if constexpr (LNM == 3)
+    epilogue_hilo_ln<K_, FM, FN>(p, acc, smem + wave * 17408, lane, m0 + wm * TM, n0 + wn * TN);
+  else if constexpr (LNM == 1)
     epilogue_acc32_wide_ln<K_, FM, FN>(p, acc, smem + wave * 8192, lane, m0 + wm * TM, n0 + wn * TN);
   else if constexpr (EACT >= EPI_ACC)
     epilogue_acc32_wide<EACT - EPI_ACC, FM, FN>(p, acc, smem + wave * SLAB, lane, m0 + wm * TM, n0 + wn * TN);
@@ -2347,6 +2485,13 @@ int launch_8ph320(const GemmP& p0, hipStream_t s) {
   const int ea = fast_epi_act(p);
   if (p.N % 256 || ea < 0 || p.relu_a) return DP_ERR_ARG;
   dim3 grid(p.tiles_n * p.tiles_m);
+  if (p.ln_xl) {         // folded-LN producer on the split (hi + lo) residual stream
+    if (!p.ln_xb_out || p.act != DP_ACT_NONE) return DP_ERR_ARG;
+    static_assert(8 * 17408 <= 2 * (320 * 128 + 256 * 128), "hi/lo staging fits the ring");
+    hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3>), grid, dim3(512), 0, s, p);
+    DP_CHECK_LAUNCH();
+    return 0;
+  }
   if (p.ln_part_out) {   // folded-LN producer: the residual accumulate
     if (ea != EPI_ACC + DP_ACT_NONE || !p.ln_xb_out) return DP_ERR_ARG;
     hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 1>), grid, dim3(512), 0, s, p);

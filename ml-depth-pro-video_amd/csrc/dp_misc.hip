@@ -124,7 +124,8 @@ int ln_launch(const float* x, long long ldx, const LnW& lw, u16* y, long long ld
 // residual GEMMs' producer epilogue writes for the rows it makes (dp_gemm_args.ln_part_out).
 template <typename K_, int VEC>
 __global__ void __launch_bounds__(256) ln_stats_kernel(const float* __restrict__ x, long long ldx, int rows,
-                                                       u16* __restrict__ xb, long long ldxb, float* __restrict__ part) {
+                                                       u16* __restrict__ xb, long long ldxb, u16* __restrict__ xl,
+                                                       float* __restrict__ part) {
   constexpr int G = VEC / 2, COLS = VEC * 256, NCH = COLS / 128;
   const int lane = threadIdx.x & 63;
   const int row = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -147,6 +148,13 @@ __global__ void __launch_bounds__(256) ln_stats_kernel(const float* __restrict__
     w.x = K_::pack2(a.x, a.y); w.y = K_::pack2(a.z, a.w);
     w.z = K_::pack2(b.x, b.y); w.w = K_::pack2(b.z, b.w);
     *(uint4*)(xb + (long long)row * ldxb + j * 512 + lane * 8) = w;
+    if (xl) {   // the split residual's low part: what the 16-bit rounding of each value dropped
+      auto lo = [](float v, uint32_t hw, int half) { return v - K_::to_f((u16)(half ? hw >> 16 : hw & 0xffff)); };
+      uint4 l;
+      l.x = K_::pack2(lo(a.x, w.x, 0), lo(a.y, w.x, 1)); l.y = K_::pack2(lo(a.z, w.y, 0), lo(a.w, w.y, 1));
+      l.z = K_::pack2(lo(b.x, w.z, 0), lo(b.y, w.z, 1)); l.w = K_::pack2(lo(b.z, w.w, 0), lo(b.w, w.w, 1));
+      *(uint4*)(xl + (long long)row * ldxb + j * 512 + lane * 8) = l;
+    }
     if ((lane & 15) == 0) {
       const int ch = j * 4 + (lane >> 4);
       *(float2*)(part + ((long long)row * NCH + ch) * 2) = make_float2(mean, q);
@@ -526,15 +534,15 @@ inline int blocks_for(long long n, int bs) { return (int)((n + bs - 1) / bs); }
 extern "C" int dp_abi_version(void) { return DP_ABI_VERSION; }
 
 extern "C" int dp_layernorm_stats(const float* x, int64_t ldx, int32_t rows, int32_t cols, void* xb, int64_t ldxb,
-                                  float* part, int32_t dtype, dp_stream_t stream) {
+                                  void* xl, float* part, int32_t dtype, dp_stream_t stream) {
   if (!x || !xb || !part) return DP_ERR_ARG;
   if (rows <= 0) return DP_ERR_SHAPE;
   if (ldx % 4 || ldxb % 8) return DP_ERR_ALIGN;
   dim3 grid((rows + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
 #define DP_LS(V_) do { \
-    if (dtype == DP_BF16) hipLaunchKernelGGL((ln_stats_kernel<KBF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, part); \
-    else if (dtype == DP_F16) hipLaunchKernelGGL((ln_stats_kernel<KF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, part); \
+    if (dtype == DP_BF16) hipLaunchKernelGGL((ln_stats_kernel<KBF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, (u16*)xl, part); \
+    else if (dtype == DP_F16) hipLaunchKernelGGL((ln_stats_kernel<KF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, (u16*)xl, part); \
     else return DP_ERR_DTYPE; } while (0)
   switch (cols) {
     case 512: DP_LS(2); break;

@@ -26,7 +26,7 @@ INTERP_MODES = {"bilinear": DP_INTERP_BILINEAR, "bicubic": DP_INTERP_BICUBIC}
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
  DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128,
  DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256, DP_TILE_SPLITK_256x256) = range(22)
-DP_ABI_VERSION = 11
+DP_ABI_VERSION = 12
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -71,7 +71,7 @@ class GemmArgs(ctypes.Structure):
         ("tile", ctypes.c_int32),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("ln_part_out", ctypes.c_void_p), ("ln_xb_out", ctypes.c_void_p), ("ln_part_in", ctypes.c_void_p),
-        ("ln_colsum", ctypes.c_void_p), ("ln_eps", ctypes.c_float),
+        ("ln_colsum", ctypes.c_void_p), ("ln_eps", ctypes.c_float), ("ln_xl", ctypes.c_void_p),
     ]
 
 
@@ -104,7 +104,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "dp_gemm_grouped": [ctypes.POINTER(GemmArgs), i32, vp],
         "dp_layernorm_grouped": [vp, i64, vp, vp, i32, vp, i64, i32, i32, f32, i32, vp],
         "dp_layernorm": [vp, i64, vp, vp, vp, i64, i32, i32, f32, i32, vp],
-        "dp_layernorm_stats": [vp, i64, i32, i32, vp, i64, vp, i32, vp],
+        "dp_layernorm_stats": [vp, i64, i32, i32, vp, i64, vp, vp, i32, vp],
         "dp_attention": [vp, vp, i32, i32, i32, i32, f32, i32, vp],
         "dp_attention_log2q": [vp, vp, i32, i32, i32, i32, i32, vp],
         "dp_normalize_u8": [vp, i32, i32, vp, i32, vp],

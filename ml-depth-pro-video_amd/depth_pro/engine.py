@@ -242,6 +242,12 @@ class _ViTBuffers:
         # folded LayerNorm: (mean, M2) of each 128-column chunk of the rows in `h` (un-normalised)
         self.part = torch.empty(rows, D // 128, 2, dtype=torch.float32, device=dev) if ln_fold else None
         self.h = torch.empty(rows, D, dtype=dt, device=dev)
+        # folded path: the residual stream between blocks is split, x = h + xl (16 bits each; the
+        # proj / fc2 epilogues read and update both, dp_gemm's ln_xl); `x` (fp32) holds it only where
+        # an fp32 reader needs it (the patch embed's output, the hooks, the final norm)
+        # (DP_LN_SPLIT=0, A/B only: the fp32 stream in `x`, read and written by every proj / fc2)
+        split = ln_fold and os.environ.get("DP_LN_SPLIT", "1") == "1"
+        self.xl = torch.empty(rows, D, dtype=dt, device=dev) if split else None
         self.qkv = torch.empty(rows, 3 * D, dtype=dt, device=dev)
         self.a = torch.empty(rows, D, dtype=dt, device=dev)
         self.m = torch.empty(rows, MLP_DIM, dtype=dt, device=dev)
@@ -551,7 +557,9 @@ class Engine:
         P = self.P
         n_img = M // TOK
         sync = sync or (lambda what, i: None)
-        ops.layernorm_stats(buf.x, buf.h, buf.part, M, D)
+        # the stream enters as fp32 (patch embed + cls rows): split it into h + xl, with the stats
+        ops.layernorm_stats(buf.x, buf.h, buf.part, M, D, xl=buf.xl)
+        split = buf.xl is not None
         yield
         for i in range(DEPTH):
             b = f"{pre}blocks.{i}."
@@ -561,15 +569,23 @@ class Engine:
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
             sync("proj", i)
-            ops.gemm(buf.a, P[b + "attn.proj.weight"], buf.x, M=M, N=D, K=D, bias=P[b + "attn.proj.bias"],
-                     gamma=P[b + "ls1.gamma"], accumulate=True, ln_out=(buf.h, buf.part))
+            ops.gemm(buf.a, P[b + "attn.proj.weight"], None if split else buf.x, M=M, N=D, K=D,
+                     bias=P[b + "attn.proj.bias"], gamma=P[b + "ls1.gamma"], accumulate=True,
+                     ln_out=(buf.h, buf.part), ln_xl=buf.xl)
             sync("fc1", i)
             ops.gemm(buf.h, P[b + "mlp.fc1.fold.w"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.fold.b"],
                      act=DP_ACT_GELU, ln_in=(buf.part, P[b + "mlp.fc1.fold.s"]))
             last = i == DEPTH - 1    # the final norm reads x itself
+            # fp32 rows only where they are read: the hooks (merge_windows) and the final norm
+            need_x = last or bool(hooks and i in hooks) or not split
             sync("fc2", i)
-            ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x, M=M, N=D, K=MLP_DIM, bias=P[b + "mlp.fc2.bias"],
-                     gamma=P[b + "ls2.gamma"], accumulate=True, ln_out=None if last else (buf.h, buf.part))
+            if split:
+                ln_out = (buf.h, None if last else buf.part)
+            else:
+                ln_out = None if last else (buf.h, buf.part)
+            ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x if need_x else None, M=M, N=D, K=MLP_DIM,
+                     bias=P[b + "mlp.fc2.bias"], gamma=P[b + "ls2.gamma"], accumulate=True,
+                     ln_out=ln_out, ln_xl=buf.xl)
             if hooks and i in hooks:
                 hooks[i]()
             if last:

@@ -152,7 +152,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          A_off: int = 0, C_off: int = 0, B_off: int = 0, tile: int = 0,
          workspace: Optional[torch.Tensor] = None,
          plan_only: bool = False, border_corr: Optional[torch.Tensor] = None,
-         ln_out: Optional[tuple] = None, ln_in: Optional[tuple] = None, ln_eps: float = 1e-6):
+         ln_out: Optional[tuple] = None, ln_in: Optional[tuple] = None, ln_eps: float = 1e-6,
+         ln_xl: Optional[torch.Tensor] = None):
     """dp_gemm. `A_off`/`B_off`/`C_off` are element offsets into A / B / C (sub-views, e.g. a
     K slice of a split-K GEMM: A_off = B_off = k0 with lda / ldb the full row lengths).
 
@@ -162,7 +163,14 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     new C rows in 16 bits to `xb` and their 128-column chunk statistics to `part`; `ln_in=(part,
     colsum)` -- A holds un-normalised 16-bit rows with statistics `part`, B / bias are folded
     (`fold_layernorm`) and `colsum` = the row sums of B.
+    Split residual (ABI 12, `ln_xl` with `ln_out=(xb, part or None)`, accumulate=True): the
+    residual stream is x = xb + ln_xl (both 16-bit), updated in place; `C` (fp32) is then only an
+    optional output of the new rows (None: not written).
     """
+    if C is None:
+        if ln_xl is None:
+            raise _lib.DPError("dp_gemm: C is required (only a split-residual producer may omit it)")
+        C = torch.empty(0, dtype=torch.float32, device=ln_xl.device)     # placeholder: C = NULL
     a = _gemm_args(A, B, C, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=ldc, conv=conv, relu_a=relu_a, bias=bias,
                    act=act, gamma=gamma, pos=pos, ldpos=ldpos, pos_group=pos_group, pos_off=pos_off, R1=R1,
                    ldr1=ldr1, R2=R2, ldr2=ldr2, accumulate=accumulate, deconv=deconv, row_group=row_group,
@@ -171,10 +179,16 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
                    border_corr=border_corr)
     if ln_out is not None:
         xb, part = ln_out
-        if xb.numel() < (M - 1) * a.ldc + N or part.numel() < M * (N // 128) * 2 or part.dtype != torch.float32 \
-                or xb.dtype != B.dtype:
+        if xb.numel() < (M - 1) * a.ldc + N or xb.dtype != B.dtype or (part is None and ln_xl is None) or \
+                (part is not None and (part.numel() < M * (N // 128) * 2 or part.dtype != torch.float32)):
             raise _lib.DPError("dp_gemm: ln_out buffers too small or of the wrong type")
-        a.ln_xb_out, a.ln_part_out = xb.data_ptr(), part.data_ptr()
+        a.ln_xb_out, a.ln_part_out = xb.data_ptr(), _p(part)
+    if ln_xl is not None:
+        if ln_out is None or ln_xl.numel() < (M - 1) * a.ldc + N or ln_xl.dtype != B.dtype:
+            raise _lib.DPError("dp_gemm: ln_xl needs ln_out and [M][ldc] 16-bit rows of the operand type")
+        a.ln_xl = ln_xl.data_ptr()
+        if C.numel() == 0:
+            a.C = None
     if ln_in is not None:
         part, colsum = ln_in
         if part.numel() < M * (K // 128) * 2 or colsum.numel() < N or colsum.dtype != torch.float32:
@@ -184,10 +198,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
         t, g = ctypes.c_int32(), ctypes.c_int32()
         check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")
         return t.value, g.value
-    _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head_w is not None, head_corr is not None, B_off)
+    _check_gemm_extents(A, B, C if a.C else None, a, A_off, C_off, conv, deconv, head_w is not None,
+                        head_corr is not None, B_off)
     kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
     with _Timed(kind, 2.0 * M * N * K, (M, N, K), B.dtype):
-        check(_lib.load().dp_gemm(ctypes.byref(a), _stream(C)), "dp_gemm")
+        check(_lib.load().dp_gemm(ctypes.byref(a), _stream(B)), "dp_gemm")
 
 
 def gemm_grouped(groups, **common) -> None:
@@ -274,6 +289,8 @@ def _check_gemm_extents(A, B, C, a, A_off, C_off, conv, deconv, head, head_ps, B
     else:
         need(A, A_off, (M - 1) * a.lda + K, "A")
     need(B, B_off, (N - 1) * a.ldb + K, "B")
+    if C is None:       # a split-residual producer with no fp32 output (its xb / xl checked by gemm)
+        return
     if head_ps:
         need(C, C_off, (M // (a.out_h * a.out_w)) * 4 * a.out_h * a.out_w, "C (pixel-shuffle head)")
     elif head:
@@ -294,13 +311,18 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, y: torch.Tensor
                                        rows, cols, eps, dtype_code(y.dtype), _stream(y)), "dp_layernorm")
 
 
-def layernorm_stats(x: torch.Tensor, xb: torch.Tensor, part: torch.Tensor, rows: int, cols: int) -> None:
+def layernorm_stats(x: torch.Tensor, xb: torch.Tensor, part: torch.Tensor, rows: int, cols: int,
+                    xl: Optional[torch.Tensor] = None) -> None:
     """dp_layernorm_stats: x (fp32 rows) -> xb (16 bits) + 128-column chunk statistics `part` --
-    the input side of a folded LayerNorm for rows no residual GEMM produced (ViT block 0)."""
+    the input side of a folded LayerNorm for rows no residual GEMM produced (ViT block 0); `xl`:
+    also the split residual's low part, x - xb in 16 bits (dp_gemm's ln_xl)."""
     if x.numel() < rows * cols or xb.numel() < rows * cols or part.numel() < rows * (cols // 128) * 2:
         raise _lib.DPError("dp_layernorm_stats: buffers smaller than rows * cols")
+    if xl is not None and (xl.numel() < rows * cols or xl.dtype != xb.dtype):
+        raise _lib.DPError("dp_layernorm_stats: xl smaller than rows * cols or not of xb's type")
     with _Timed("layernorm", 0.0, (rows, cols), xb.dtype):
-        check(_lib.load().dp_layernorm_stats(x.data_ptr(), cols, rows, cols, xb.data_ptr(), cols, part.data_ptr(),
+        check(_lib.load().dp_layernorm_stats(x.data_ptr(), cols, rows, cols, xb.data_ptr(), cols,
+                                             xl.data_ptr() if xl is not None else None, part.data_ptr(),
                                              dtype_code(xb.dtype), _stream(xb)), "dp_layernorm_stats")
 
 

@@ -175,7 +175,7 @@ def test_empty_inputs_are_refused_before_launch():
         "attention seq=0": lambda: lib.dp_attention(P, P, 1, 0, 16, 64, f32(0.125), 0, None),
         "attention_log2q heads=0": lambda: lib.dp_attention_log2q(P, P, 1, 577, 0, 64, 0, None),
         "layernorm rows=0": lambda: lib.dp_layernorm(P, 1024, P, P, P, 1024, 0, 1024, f32(1e-6), 0, None),
-        "layernorm_stats rows=0": lambda: lib.dp_layernorm_stats(P, 1024, 0, 1024, P, 1024, P, 0, None),
+        "layernorm_stats rows=0": lambda: lib.dp_layernorm_stats(P, 1024, 0, 1024, P, 1024, None, P, 0, None),
         "normalize_u8 H=0": lambda: lib.dp_normalize_u8(P, 0, 100, P, 0, None),
         "resize_bilinear OH=0": lambda: lib.dp_resize_bilinear(P, 0, 3, 10, 10, P, 0, 10, None),
         "resize H=0": lambda: lib.dp_resize(P, 0, 3, 0, 10, P, 10, 10, 0, None),

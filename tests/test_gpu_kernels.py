@@ -1019,6 +1019,69 @@ def test_gemm_8ph320_ln_producer(cuda, dt, M, K):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+def test_layernorm_stats_split_residual(cuda, dt):
+    """dp_layernorm_stats with xl (ABI 12): xb == x in 16 bits, xl == (x - xb) in 16 bits, so that
+    xb + xl carries x to ~17 significant bits (the split residual's entry into ViT block 0)."""
+    g = torch.Generator().manual_seed(12)
+    rows = 1155
+    x = torch.randn(rows, 1024, generator=g) * 3 + torch.randn(rows, 1, generator=g) * 2
+    xb = torch.empty(rows, 1024, dtype=dt, device=cuda)
+    xl = torch.empty(rows, 1024, dtype=dt, device=cuda)
+    part = torch.empty(rows, 8, 2, device=cuda)
+    ops.layernorm_stats(x.to(cuda), xb, part, rows, 1024, xl=xl)
+    hi = x.to(dt)
+    assert torch.equal(xb.cpu(), hi)
+    assert torch.equal(xl.cpu(), (x - hi.float()).to(dt))
+    rel = ((xb.cpu().float() + xl.cpu().float() - x).abs() / x.abs().clamp_min(1e-3)).max().item()
+    assert rel < (2e-5 if dt == torch.bfloat16 else 2e-6), rel
+    np.testing.assert_allclose(part.cpu().double().numpy(), _chunk_stats(x).numpy(), rtol=2e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,K,fp32_out,with_part", [(20195, 1024, False, True), (577, 4096, True, True),
+                                                     (20195, 4096, True, False)])
+def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part):
+    """Folded-LN producer on the split residual (ABI 12, dp_gemm ln_xl; the ViT proj / fc2): with the
+    stream given as hi + lo, the new rows are bit-identical to the fp32 producer's on C = hi + lo
+    (same per-element operation order): C (when asked for) equal, hi == C in 16 bits, lo == (C - hi)
+    in 16 bits, part equal; rows past M untouched (M = 20195: a 35-row last tile)."""
+    g = torch.Generator().manual_seed(M + K + 7)
+    N = 1024
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    gamma = (0.1 + 0.02 * torch.randn(N, generator=g)).to(cuda)
+    x = torch.randn(M, N, generator=g) * 2 + 0.5
+    hi0 = x.to(dt)
+    lo0 = (x - hi0.float()).to(dt)
+    C1 = (hi0.float() + lo0.float()).to(cuda)            # the fp32 producer's input: exactly hi + lo
+    xb1 = torch.empty(M, N, dtype=dt, device=cuda)
+    part1 = torch.empty(M, N // 128, 2, device=cuda)
+    kw = dict(M=M, N=N, K=K, bias=bias, gamma=gamma, accumulate=True)
+    ops.gemm(A, B, C1, ln_out=(xb1, part1), **kw)
+    # split: hi / lo with a guard row past M on each (must stay untouched)
+    hi = torch.empty(M + 1, N, dtype=dt, device=cuda)
+    lo = torch.empty(M + 1, N, dtype=dt, device=cuda)
+    hi[:M], lo[:M] = hi0.to(cuda), lo0.to(cuda)
+    hi[M], lo[M] = 7.0, -3.0
+    part = torch.full((M, N // 128, 2), 123.0, device=cuda) if with_part else None
+    C2 = torch.full((M, N), 5.0, device=cuda) if fp32_out else None
+    tile, _ = ops.gemm(A, B, C2, plan_only=True, ln_out=(hi, part), ln_xl=lo, **kw)
+    from depth_pro._lib import DP_TILE_8PH_320x256
+
+    assert tile == DP_TILE_8PH_320x256
+    ops.gemm(A, B, C2, ln_out=(hi, part), ln_xl=lo, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(hi[:M], xb1)
+    assert torch.equal(lo[:M], (C1 - xb1.float()).to(dt))
+    assert torch.all(hi[M] == 7.0) and torch.all(lo[M] == -3.0)
+    if fp32_out:
+        assert torch.equal(C2, C1)
+    if with_part:
+        assert torch.equal(part, part1)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act,col_scale,engine", [(0, True, "8ph320"), (DP_ACT_GELU, False, "8ph320"),
                                                   (DP_ACT_GELU, False, "p8ph")])
 def test_gemm_8ph320_ln_consumer(cuda, dt, act, col_scale, engine):

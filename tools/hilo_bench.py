@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""proj / fc2 residual GEMMs (the folded-LN producers, M = 20195, N = 1024) with the fp32 residual
+stream vs the split (hi + lo 16-bit) one: average launch time, warm (operands re-used, the stream
+resident in the Infinity Cache) and cold (a 512 MB write between launches evicts it, as the frame's
+other kernels do)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
+from depth_pro import ops  # noqa: E402
+
+
+def timeit(fn, iters, flush=None):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    tot = 0.0
+    for _ in range(iters):
+        if flush is not None:
+            flush()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        tot += e0.elapsed_time(e1)
+    return 1000.0 * tot / iters
+
+
+def main():
+    dev = torch.device("cuda:0")
+    dt = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(0)
+    M, N = 20195, 1024
+    junk = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    flush = lambda: junk.fill_(1)  # noqa: E731
+    x = torch.randn(M, N, device=dev, generator=g) * 2
+    hi = x.to(dt)
+    lo = (x - hi.float()).to(dt)
+    part = torch.empty(M, N // 128, 2, device=dev)
+    for name, K in (("proj", 1024), ("fc2", 4096)):
+        A = torch.randn(M, K, device=dev, generator=g).to(dt)
+        B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
+        bias = torch.randn(N, device=dev, generator=g)
+        gamma = torch.full((N,), 1e-3, device=dev)
+        kw = dict(M=M, N=N, K=K, bias=bias, gamma=gamma, accumulate=True)
+        xb = torch.empty(M, N, dtype=dt, device=dev)
+        f32 = lambda: ops.gemm(A, B, x, ln_out=(xb, part), **kw)  # noqa: E731
+        spl = lambda: ops.gemm(A, B, None, ln_out=(hi, part), ln_xl=lo, **kw)  # noqa: E731
+        flop = 2.0 * M * N * K
+        res = []
+        for lab, fn in (("fp32", f32), ("split", spl)):
+            for cl, fl in (("warm", None), ("cold", flush)):
+                us = timeit(fn, 20, fl)
+                res.append(f"{lab}/{cl} {us:7.1f}us {flop / us / 1e6:6.1f}TF")
+        print(f"{name:5s} " + " | ".join(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
