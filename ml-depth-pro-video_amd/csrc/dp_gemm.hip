@@ -122,7 +122,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   if (lnc && (!a->ln_part_in || !a->ln_colsum || a->K != 1024 || a->accumulate || a->c_dtype == DP_F32 ||
               a->gamma || (a->act != DP_ACT_NONE && a->act != DP_ACT_GELU) || !(a->ln_eps > 0.f)))
     return DP_ERR_ARG;
-  if ((lnp || lnc) && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_8PH_320x256) return DP_ERR_ARG;
+  if ((lnp || lnc) && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_8PH_320x256 &&
+      !(lnc && a->tile == DP_TILE_P8PH_256x256))   // (a consumer may ask for the persistent engine)
+    return DP_ERR_ARG;
   const bool ws_ok = a->workspace && a->workspace_bytes >= dp_gemm_workspace_size();
   const int dbg = g_dbg_flags.load(std::memory_order_relaxed);
   tile = a->tile;

@@ -1032,6 +1032,25 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
       : "memory");
 }
 
+// LDS image of one operand tile: rows of BKT 16-bit elements (64 or 128 B), the
+// 16-B chunk index XOR-swizzled so that the 16 rows one ds_read_b128 lane group
+// reads hit 16 distinct bank slots (conflict-free, checked with SQ_LDS_BANK_CONFLICT).
+template <int BKT>
+__device__ __forceinline__ int lds_off_t(int row, int chunk) {
+  if constexpr (BKT == 64) return row * 64 + ((chunk ^ (row & 7)) << 3);
+  else return row * 32 + ((chunk ^ ((row >> 1) & 3)) << 3);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n <= N, n a multiple of step
+  if constexpr (N == 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N) wait_vmcnt<N>();
+    else wait_vmcnt_le<N - 1>(n);
+  }
+}
+
 // Folded-LN producer on a SPLIT residual stream (dp_gemm_args.ln_xl, LNM = 3 of the 8-phase
 // 320 x 256 engine): the ViT residual x is held as two 16-bit arrays, x = hi + lo, hi =
 // ln_xb_out (the next GEMM's A operand anyway) and lo = ln_xl (what hi's rounding dropped, itself
@@ -1041,20 +1060,32 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
 // operation order), hi' = r16(x'), lo' = r16(x' - hi'); (mean, M2) of each row's 128 columns as
 // epilogue_acc32_wide_ln (when ln_part_out); C (fp32) = x' when given (never read).  8 B of HBM
 // per element instead of 10 (fp32 read + write, 16-bit hi write): the epilogue of a one-round
-// launch (proj / fc2) is HBM-bound.
-// Per 16-row fragment row fm: the wave's hi and lo rows (16 x 128 x 16 bit each) arrive by
-// LDS-DMA one fragment row ahead into a 2-deep per-wave staging ring (16-B chunks XOR-swizzled by
-// row on the source address: the MFMA-layout reads are conflict-free), are read in the MFMA
-// layout, updated in place, read back as rows and leave as 256-B row segments.  Every store is a
-// buffer store whose masked lanes (rows past M, an absent output) carry an out-of-range offset, so
-// each iteration issues a fixed number of VMEM instructions (ST below) and the counted wait for a
-// fragment row's DMA is a compile-time constant.  `slab`: the wave's LDS region, >= 17 KiB.
-template <typename K_, int FM, int FN>
+// launch (proj / fc2) is HBM-bound (proj 85 -> 75, fc2 172 -> 161 us, profiles/r05a_split_residual).
+// The epilogue is bound by the bytes in flight (8 waves per CU, nothing else to run): it walks the
+// wave's 80 x 128 outputs in NI = 10 chunks of 16 rows x 64 columns (fragment row fm, column half
+// h), whose hi and lo rows (2 KiB each) arrive by LDS-DMA THREE chunks ahead into a 4-deep
+// per-wave ring (16 KiB; the 16-B chunks XOR-swizzled by row pair on the source address, so the
+// MFMA-layout reads are conflict-free), are read in the MFMA layout, updated in place, read back
+// as rows and leave as 128-B row segments.  Every store is a buffer store whose masked lanes (rows
+// past M, an absent output) carry an out-of-range offset, so each chunk issues a fixed number of
+// VMEM instructions (st(i) below) and the counted wait for a chunk's DMA is a compile-time
+// constant.  `slab`: the wave's LDS region, >= 17 KiB.
+// (AHEAD = 1: one chunk in flight, the A/B variant behind debug 1 << 27: proj 75 vs ? us)
+template <typename K_, int FM, int FN, int AHEAD = 3>
 __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[FM][FN], char* slab, int lane,
                                                  int m_base, int n_base) {
   #pragma clang fp contract(off)
-  static_assert(FN == 8, "128 columns per wave");
-  constexpr int ST = 8 + 1 + 8;       // VMEM stores per fragment row: C (8 x 16 B), part, hi + lo rows (8)
+  static_assert(FN == 8 && AHEAD >= 1 && AHEAD <= 3, "128 columns per wave, <= 4 ring slots");
+  constexpr int NI = 2 * FM, CB = 4096;   // chunks, ring slot bytes (hi | lo)
+  // VMEM instructions a chunk issues: C (4 x 16 B per lane), part (second half only), hi + lo rows (2 + 2)
+  constexpr auto st = [](int i) constexpr { return 4 + (i & 1) + 4; };
+  // the counted wait for chunk i's DMA: younger are the DMAs of chunks i+1 .. i+AHEAD (4 pieces each)
+  // and the stores of the chunks processed since chunk i's DMA was issued
+  constexpr auto younger = [](int i) constexpr {
+    int n = 4 * ((i + AHEAD < NI - 1 ? i + AHEAD : NI - 1) - i);
+    for (int j = (i - AHEAD > 0 ? i - AHEAD : 0); j < i; ++j) n += 4 + (j & 1) + 4;
+    return n;
+  };
   const int t = lane & 15, g = lane >> 4;
   {
     const int c = 4 * (lane & 31), n = n_base + c;
@@ -1064,9 +1095,9 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
     *(f32x4_t*)(slab + (lane < 32 ? 0 : 512) + c * 4) = v;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the constants, before any DMA is counted
+  constexpr unsigned OOB = 0xFFFFFFF0u;   // a masked store's offset: past every extent (host: < 0xFFFFFF00)
   const u16* const hi_in = p.ln_xb_out;
   const u16* const lo_in = p.ln_xl;
-  constexpr unsigned OOB = 0xFFFFFFF0u;   // a masked store's offset: past every extent (host: < 0xFFFFFF00)
   const unsigned row_b = (unsigned)(p.M * p.ldc * 2);              // bytes of hi / lo
   const __amdgpu_buffer_rsrc_t rs_hi = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_xb_out, (short)0, (int)row_b, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_lo = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_xl, (short)0, (int)row_b, 0x00020000);
@@ -1077,37 +1108,39 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
       p.ln_part_out ? (void*)p.ln_part_out : (void*)p.ln_xl, (short)0, p.ln_part_out ? (int)(p.M * nch * 8) : 0,
       0x00020000);
   const uint32_t slab_lds = __builtin_amdgcn_readfirstlane(lds_addr(slab)) + 1024;
-  // DMA of fragment row fm's hi / lo rows into staging buffer b: piece pc of an array = rows
-  // pc * 4 + lane / 16, 16 lanes x 16 B per 256-B row, logical chunk (lane & 15) ^ row
-  auto dma = [&](int fm, int b) __attribute__((always_inline)) {
+  // chunk i = (fm, h): rows fm * 16 .. + 15, columns h * 64 .. + 63 of the wave's range; ring slot
+  // i & 3: hi rows [16][128 B] then lo rows; piece pc of an array = rows pc * 8 + lane / 8, 8 lanes
+  // x 16 B per 128-B row, physical 16-B chunk lane & 7 = logical chunk (lane & 7) ^ ((row >> 1) & 7)
+  auto dma = [&](int i) __attribute__((always_inline)) {
+    const int fm = i >> 1, h = i & 1;
     #pragma unroll
-    for (int pc = 0; pc < 4; ++pc) {
-      const int r = pc * 4 + (lane >> 4);
+    for (int pc = 0; pc < 2; ++pc) {
+      const int r = pc * 8 + (lane >> 3);
       const int m = min(m_base + fm * 16 + r, p.M - 1);
-      const long long o = (long long)m * p.ldc + n_base + (((lane & 15) ^ r) << 3);
-      glds16(hi_in + o, slab_lds + b * 8192 + pc * 1024);
-      glds16(lo_in + o, slab_lds + b * 8192 + 4096 + pc * 1024);
+      const long long o = (long long)m * p.ldc + n_base + h * 64 + (((lane & 7) ^ ((r >> 1) & 7)) << 3);
+      glds16(hi_in + o, slab_lds + (i & 3) * CB + pc * 1024);
+      glds16(lo_in + o, slab_lds + (i & 3) * CB + 2048 + pc * 1024);
     }
   };
-  dma(0, 0);
   #pragma unroll
-  for (int fm = 0; fm < FM; ++fm) {
-    char* const buf = slab + 1024 + (fm & 1) * 8192;
-    if (fm + 1 < FM) dma(fm + 1, (fm + 1) & 1);
-    // fragment row fm's DMA landed: younger are the previous row's ST stores and the next DMA
-    if (fm == 0) { if (FM > 1) wait_vmcnt<8>(); else wait_vmcnt<0>(); }
-    else if (fm + 1 < FM) wait_vmcnt<ST + 8>();
-    else wait_vmcnt<ST>();
+  for (int i = 0; i < AHEAD && i < NI; ++i) dma(i);
+  float sh = 0.f, s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int fm = i >> 1, h = i & 1;
+    char* const buf = slab + 1024 + (i & 3) * CB;
+    if (i + AHEAD < NI) dma(i + AHEAD);
+    wait_vmcnt_le<48>(younger(i));   // a constant once the loop is unrolled
     const int m = m_base + fm * 16 + t;
     const bool mok = m < p.M;
-    float sh = 0.f, s1 = 0.f, s2 = 0.f;
     #pragma unroll
-    for (int fn = 0; fn < FN; ++fn) {
-      const int off = t * 256 + (((fn * 2 + (g >> 1)) ^ t) << 4) + (g & 1) * 8;
-      const uint2 h = *(const uint2*)(buf + off);
-      const uint2 l = *(const uint2*)(buf + 4096 + off);
-      const float xin[4] = {K_::to_f(h.x & 0xffff) + K_::to_f(l.x & 0xffff), K_::to_f(h.x >> 16) + K_::to_f(l.x >> 16),
-                            K_::to_f(h.y & 0xffff) + K_::to_f(l.y & 0xffff), K_::to_f(h.y >> 16) + K_::to_f(l.y >> 16)};
+    for (int f = 0; f < 4; ++f) {
+      const int fn = h * 4 + f;
+      const int off = t * 128 + (((f * 2 + (g >> 1)) ^ ((t >> 1) & 7)) << 4) + (g & 1) * 8;
+      const uint2 hv = *(const uint2*)(buf + off);
+      const uint2 lv = *(const uint2*)(buf + 2048 + off);
+      const float xin[4] = {K_::to_f(hv.x & 0xffff) + K_::to_f(lv.x & 0xffff), K_::to_f(hv.x >> 16) + K_::to_f(lv.x >> 16),
+                            K_::to_f(hv.y & 0xffff) + K_::to_f(lv.y & 0xffff), K_::to_f(hv.y >> 16) + K_::to_f(lv.y >> 16)};
       const f32x4_t b = *(const f32x4_t*)(slab + (fn * 16 + 4 * g) * 4);
       const f32x4_t q = *(const f32x4_t*)(slab + 512 + (fn * 16 + 4 * g) * 4);
       f32x4_t x;
@@ -1136,14 +1169,14 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
       wl.x = K_::pack2(x[0] - K_::to_f(wh.x & 0xffff), x[1] - K_::to_f(wh.x >> 16));
       wl.y = K_::pack2(x[2] - K_::to_f(wh.y & 0xffff), x[3] - K_::to_f(wh.y >> 16));
       *(uint2*)(buf + off) = wh;
-      *(uint2*)(buf + 4096 + off) = wl;
+      *(uint2*)(buf + 2048 + off) = wl;
     }
-    // the row's 128 columns: 4 lanes (g) of 32 values each
-    s1 += __shfl_xor(s1, 16);
-    s2 += __shfl_xor(s2, 16);
-    s1 += __shfl_xor(s1, 32);
-    s2 += __shfl_xor(s2, 32);
-    {
+    if (h == 1) {
+      // the row's 128 columns: 4 lanes (g) of 32 values each
+      s1 += __shfl_xor(s1, 16);
+      s2 += __shfl_xor(s2, 16);
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
       const float mc = sh + s1 * (1.f / 128);
       const float m2 = s2 - s1 * (s1 * (1.f / 128));
       const unsigned po = (g == 0 && mok) ? (unsigned)(((long long)m * nch + n_base / 128) * 8) : OOB;
@@ -1151,39 +1184,21 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's staging writes
     #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int row = k * 4 + (lane >> 4), chunk = lane & 15;
-      const int o = row * 256 + ((chunk ^ row) << 4);
+    for (int k = 0; k < 2; ++k) {
+      const int row = k * 8 + (lane >> 3), chunk = lane & 7;
+      const int o = row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
       const uint4 dh = *(const uint4*)(buf + o);
-      const uint4 dl = *(const uint4*)(buf + 4096 + o);
+      const uint4 dl = *(const uint4*)(buf + 2048 + o);
       const int mm = m_base + fm * 16 + row;
-      const unsigned bo = mm < p.M ? (unsigned)(((long long)mm * p.ldc + n_base + chunk * 8) * 2) : OOB;
+      const unsigned bo = mm < p.M ? (unsigned)(((long long)mm * p.ldc + n_base + h * 64 + chunk * 8) * 2) : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{dh.x, dh.y, dh.z, dh.w}, rs_hi, bo, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{dl.x, dl.y, dl.z, dl.w}, rs_lo, bo, 0, 0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read back before this buffer's next DMA
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read back before this slot's next DMA
   }
+  (void)st;
 }
 
-
-// LDS image of one operand tile: rows of BKT 16-bit elements (64 or 128 B), the
-// 16-B chunk index XOR-swizzled so that the 16 rows one ds_read_b128 lane group
-// reads hit 16 distinct bank slots (conflict-free, checked with SQ_LDS_BANK_CONFLICT).
-template <int BKT>
-__device__ __forceinline__ int lds_off_t(int row, int chunk) {
-  if constexpr (BKT == 64) return row * 64 + ((chunk ^ (row & 7)) << 3);
-  else return row * 32 + ((chunk ^ ((row >> 1) & 3)) << 3);
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n <= N, n a multiple of step
-  if constexpr (N == 0) {
-    wait_vmcnt<0>();
-  } else {
-    if (n >= N) wait_vmcnt<N>();
-    else wait_vmcnt_le<N - 1>(n);
-  }
-}
 
 // NW = waves per workgroup: 8 (one workgroup per CU), or 4 (two workgroups per CU, each
 // wave one per SIMD: one workgroup's epilogue runs beside the other's K loop).
@@ -2339,7 +2354,7 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
 // s+1 in phase 3 -- so each piece has 4+ phases to land and the count is 8 in steady state.
 // Dense A only; epilogues: the load-free MFMA-layout one (EACT = DP_ACT_*; 16-bit C) or the
 // fp32 residual-accumulate one (EACT = EPI_ACC + act).
-template <typename K_, int EACT, int LNM = 0>   // LNM: 1 folded-LN producer, 2 consumer, 3 producer on hi + lo
+template <typename K_, int EACT, int LNM = 0>   // LNM: 1 folded-LN producer, 2 consumer, 3 (4) producer on hi + lo
 __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   constexpr int BM = 320;
   constexpr int A_BYTES = BM * 128, B_BYTES = 256 * 128, BUF = A_BYTES + B_BYTES;
@@ -2467,6 +2482,8 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   lds_barrier();   // the ring is free once every wave has left the K loop
   if constexpr (LNM == 3)
     epilogue_hilo_ln<K_, FM, FN>(p, acc, smem + wave * 17408, lane, m0 + wm * TM, n0 + wn * TN);
+  else if constexpr (LNM == 4)
+    epilogue_hilo_ln<K_, FM, FN, 1>(p, acc, smem + wave * 17408, lane, m0 + wm * TM, n0 + wn * TN);
   else if constexpr (LNM == 1)
     epilogue_acc32_wide_ln<K_, FM, FN>(p, acc, smem + wave * 8192, lane, m0 + wm * TM, n0 + wn * TN);
   else if constexpr (EACT >= EPI_ACC)
@@ -2488,7 +2505,8 @@ int launch_8ph320(const GemmP& p0, hipStream_t s) {
   if (p.ln_xl) {         // folded-LN producer on the split (hi + lo) residual stream
     if (!p.ln_xb_out || p.act != DP_ACT_NONE) return DP_ERR_ARG;
     static_assert(8 * 17408 <= 2 * (320 * 128 + 256 * 128), "hi/lo staging fits the ring");
-    hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3>), grid, dim3(512), 0, s, p);
+    if (p.dbg & (1 << 27)) hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 4>), grid, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3>), grid, dim3(512), 0, s, p);
     DP_CHECK_LAUNCH();
     return 0;
   }

@@ -1041,9 +1041,9 @@ def test_layernorm_stats_split_residual(cuda, dt):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
-@pytest.mark.parametrize("M,K,fp32_out,with_part", [(20195, 1024, False, True), (577, 4096, True, True),
-                                                     (20195, 4096, True, False)])
-def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part):
+@pytest.mark.parametrize("M,K,fp32_out,with_part,dbg", [(20195, 1024, False, True, 0), (577, 4096, True, True, 0),
+                                                         (20195, 4096, True, False, 0), (20195, 1024, True, True, 1 << 27)])
+def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part, dbg):
     """Folded-LN producer on the split residual (ABI 12, dp_gemm ln_xl; the ViT proj / fc2): with the
     stream given as hi + lo, the new rows are bit-identical to the fp32 producer's on C = hi + lo
     (same per-element operation order): C (when asked for) equal, hi == C in 16 bits, lo == (C - hi)
@@ -1070,11 +1070,16 @@ def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part
     part = torch.full((M, N // 128, 2), 123.0, device=cuda) if with_part else None
     C2 = torch.full((M, N), 5.0, device=cuda) if fp32_out else None
     tile, _ = ops.gemm(A, B, C2, plan_only=True, ln_out=(hi, part), ln_xl=lo, **kw)
+    from depth_pro import _lib
     from depth_pro._lib import DP_TILE_8PH_320x256
 
     assert tile == DP_TILE_8PH_320x256
-    ops.gemm(A, B, C2, ln_out=(hi, part), ln_xl=lo, **kw)
-    torch.cuda.synchronize()
+    _lib.load().dp_gemm_debug_flags(dbg)      # 1 << 27: the one-chunk-ahead epilogue (A/B variant)
+    try:
+        ops.gemm(A, B, C2, ln_out=(hi, part), ln_xl=lo, **kw)
+        torch.cuda.synchronize()
+    finally:
+        _lib.load().dp_gemm_debug_flags(0)
     assert torch.equal(hi[:M], xb1)
     assert torch.equal(lo[:M], (C1 - xb1.float()).to(dt))
     assert torch.all(hi[M] == 7.0) and torch.all(lo[M] == -3.0)

@@ -51,10 +51,14 @@ def main():
         spl = lambda: ops.gemm(A, B, None, ln_out=(hi, part), ln_xl=lo, **kw)  # noqa: E731
         flop = 2.0 * M * N * K
         res = []
-        for lab, fn in (("fp32", f32), ("split", spl)):
+        from depth_pro import _lib
+        lib = _lib.load()
+        for lab, fn, dbg in (("fp32", f32, 0), ("split", spl, 0), ("split-ahead1", spl, 1 << 27)):
+            lib.dp_gemm_debug_flags(dbg)
             for cl, fl in (("warm", None), ("cold", flush)):
                 us = timeit(fn, 20, fl)
                 res.append(f"{lab}/{cl} {us:7.1f}us {flop / us / 1e6:6.1f}TF")
+        lib.dp_gemm_debug_flags(0)
         print(f"{name:5s} " + " | ".join(res), flush=True)
 
 
