@@ -133,13 +133,16 @@ typedef struct dp_gemm_args {
    *      v = rstd * acc - rstd * mean * ln_colsum[n] + bias[n]
    *    with (mean, rstd) of the row merged from its K/128 chunks: LN(x) . W^T + b exactly, up
    *    to where the 16-bit rounding falls (x instead of LN(x)).
-   *  producer on a SPLIT residual (ABI 12, ln_xl != NULL): the residual stream is held as two
-   *    16-bit arrays (dtype, [M][ldc]), x = ln_xb_out + ln_xl, read and updated in place:
-   *    x' = v + x;  ln_xb_out = x' rounded to 16 bits;  ln_xl = (x' - ln_xb_out) rounded to 16 bits
-   *    (~17 significant bits: the fp32 stream's error unchanged, tools/hilo_emul.py); ln_part_out
-   *    as above or NULL; C (fp32, [M][ldc]) is not read: NULL, or written with x' (for a reader of
-   *    the fp32 rows); accumulate = 1, act none, N % 128 == 0, M * ldc * 4 < 2^32 - 256.  8 instead
-   *    of 10 bytes of HBM traffic per element in a residual GEMM's epilogue. */
+   *  producer on a SPLIT residual (ABI 12, ln_xl != NULL): the residual stream is held as a 16-bit
+   *    high part (ln_xb_out, dtype, [M][ldc]) and an int8 low part (ln_xl, [M][ldc] bytes), read and
+   *    updated in place:  x = hi + q * 2^(e - S)  with e the frexp exponent of hi (hi = m 2^e,
+   *    m in [0.5, 1)), S = 16 (bf16) / 19 (f16), i.e. q counts steps of ulp(hi) / 256;
+   *    x' = v + x;  hi' = x' rounded to 16 bits;  q' = clamp(rint((x' - hi') 2^(S - e')), -128, 127)
+   *    (~16 significant bits: the patch encoder's error vs fp32 moves 2.3788e-3 -> 2.3809e-3,
+   *    tools/hilo_emul.py); ln_part_out as above or NULL; C (fp32, [M][ldc]) is not read: NULL, or
+   *    written with x' (for a reader of the fp32 rows); accumulate = 1, act none, N % 128 == 0,
+   *    M * ldc * 4 < 2^32 - 256.  6 instead of 10 bytes of HBM traffic per element in a residual
+   *    GEMM's epilogue. */
   float* ln_part_out;
   void* ln_xb_out;
   const float* ln_part_in;
@@ -231,8 +234,9 @@ int dp_layernorm(const float* x, int64_t ldx, const float* w, const float* b, vo
  * fp32 x [rows][cols] (cols % 128 == 0, <= 2048) write x in 16 bits (xb [rows][ldxb], dtype) and
  * part fp32 [rows][cols/128][2] = (mean, M2) of each 128-column chunk -- what the residual GEMMs'
  * producer epilogue writes, for the rows no GEMM produced (the patch embed + cls rows that enter
- * ViT block 0).  xl (ABI 12; NULL: none): the low part of the split residual, (x - xb) in 16 bits
- * ([rows][ldxb]), so that xb + xl is the stream a split-residual producer (dp_gemm_args.ln_xl) reads.
+ * ViT block 0).  xl (ABI 12; NULL: none): the int8 low part of the split residual ([rows][ldxb]
+ * bytes, the encoding of dp_gemm_args.ln_xl), so that (xb, xl) is the stream a split-residual
+ * producer reads.
  */
 int dp_layernorm_stats(const float* x, int64_t ldx, int32_t rows, int32_t cols, void* xb, int64_t ldxb,
                        void* xl, float* part, int32_t dtype, dp_stream_t stream);

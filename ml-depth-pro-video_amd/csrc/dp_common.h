@@ -19,6 +19,7 @@ typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
 // the kind only decides the MFMA opcode and the float<->16-bit conversions.
 struct KBF16 {
   static constexpr int id = DP_BF16;
+  static constexpr int lo8_shift = 7 + 9;      // split residual (lo8_*): 2^(e - 16) = ulp(hi) / 256
   static __device__ __forceinline__ float to_f(u16 v) {
     return __uint_as_float(((uint32_t)v) << 16);
   }
@@ -41,6 +42,7 @@ struct KBF16 {
 
 struct KF16 {
   static constexpr int id = DP_F16;
+  static constexpr int lo8_shift = 10 + 9;     // 2^(e - 19) = ulp(hi) / 256
   static __device__ __forceinline__ float to_f(u16 v) {
     return (float)__builtin_bit_cast(_Float16, v);
   }
@@ -59,6 +61,27 @@ struct KF16 {
                                                   __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
   }
 };
+
+// The split residual's 8-bit low part (dp_gemm_args.ln_xl, ABI 12): x = hi + q * 2^(e - S), hi = x
+// rounded to 16 bits, e = frexp exponent of hi (hi = m 2^e, m in [0.5, 1)), S = K_::lo8_shift, so
+// the step is ulp(hi) / 256 and q = rint((x - hi) / step) in [-128, 127] (|x - hi| <= ulp / 2: only
+// an exact tie reaches 128, clamped).  x - hi, the scaling and hi + q step are exact in fp32, so
+// host code reproduces both directions bit for bit.  About 16 significant bits of x.
+template <typename K_>
+__device__ __forceinline__ int lo8_encode(float x, float hf) {
+  const int e = __builtin_amdgcn_frexp_expf(hf);
+  const float q = __builtin_rintf(__builtin_amdgcn_ldexpf(x - hf, K_::lo8_shift - e));
+  return (int)__builtin_amdgcn_fmed3f(q, -128.f, 127.f);
+}
+template <typename K_>
+__device__ __forceinline__ float lo8_decode(float hf, int q) {
+  return hf + __builtin_amdgcn_ldexpf((float)q, __builtin_amdgcn_frexp_expf(hf) - K_::lo8_shift);
+}
+// 4 signed bytes <-> 4 ints (byte r = value r)
+__device__ __forceinline__ uint32_t pack_i8x4(int a, int b, int c, int d) {
+  return (uint32_t)(a & 0xff) | ((uint32_t)(b & 0xff) << 8) | ((uint32_t)(c & 0xff) << 16) | ((uint32_t)d << 24);
+}
+__device__ __forceinline__ int unpack_i8(uint32_t w, int r) { return (int)(w << (24 - 8 * r)) >> 24; }
 
 // ReLU on packed 16-bit floats (bf16 or f16): a negative value has its sign bit
 // set, i.e. is a negative int16, so max_i16(x, 0) zeroes it (-0 and negative

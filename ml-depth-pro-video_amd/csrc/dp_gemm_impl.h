@@ -1052,38 +1052,37 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {  // s_waitcnt vmcnt(n), n
 }
 
 // Folded-LN producer on a SPLIT residual stream (dp_gemm_args.ln_xl, LNM = 3 of the 8-phase
-// 320 x 256 engine): the ViT residual x is held as two 16-bit arrays, x = hi + lo, hi =
-// ln_xb_out (the next GEMM's A operand anyway) and lo = ln_xl (what hi's rounding dropped, itself
-// rounded to 16 bits: about 17 significant bits against fp32's 24 -- the patch encoder's rel-L1
-// vs the fp32 reference 2.3789e-3 against 2.3788e-3 with an fp32 stream, bf16 hi alone 1.06e-2,
-// tools/hilo_emul.py).  Per element: x' = (acc + b) * gamma + (hi + lo) (the fp32 epilogue's
-// operation order), hi' = r16(x'), lo' = r16(x' - hi'); (mean, M2) of each row's 128 columns as
-// epilogue_acc32_wide_ln (when ln_part_out); C (fp32) = x' when given (never read).  8 B of HBM
-// per element instead of 10 (fp32 read + write, 16-bit hi write): the epilogue of a one-round
-// launch (proj / fc2) is HBM-bound (proj 85 -> 75, fc2 172 -> 161 us, profiles/r05a_split_residual).
-// The epilogue is bound by the bytes in flight (8 waves per CU, nothing else to run): it walks the
-// wave's 80 x 128 outputs in NI = 10 chunks of 16 rows x 64 columns (fragment row fm, column half
-// h), whose hi and lo rows (2 KiB each) arrive by LDS-DMA THREE chunks ahead into a 4-deep
-// per-wave ring (16 KiB; the 16-B chunks XOR-swizzled by row pair on the source address, so the
-// MFMA-layout reads are conflict-free), are read in the MFMA layout, updated in place, read back
-// as rows and leave as 128-B row segments.  Every store is a buffer store whose masked lanes (rows
-// past M, an absent output) carry an out-of-range offset, so each chunk issues a fixed number of
-// VMEM instructions (st(i) below) and the counted wait for a chunk's DMA is a compile-time
-// constant.  `slab`: the wave's LDS region, >= 17 KiB.
-// (AHEAD = 1: one chunk in flight, the A/B variant behind debug 1 << 27: proj 75 vs ? us)
+// 320 x 256 engine): the ViT residual x is held as hi (16 bits, = ln_xb_out, the next GEMM's A
+// operand anyway) and an 8-bit low part (ln_xl: x - hi in steps of ulp(hi) / 256, lo8_encode):
+// about 16 significant bits against fp32's 24 -- the patch encoder's rel-L1 vs the fp32 reference
+// 2.3809e-3 against 2.3788e-3 with an fp32 stream (a 16-bit low part 2.3789e-3, bf16 hi alone
+// 1.06e-2; tools/hilo_emul.py).  Per element: x' = (acc + b) * gamma + (hi + lo) (the fp32
+// epilogue's operation order), hi' = r16(x'), lo' = lo8(x', hi'); (mean, M2) of each row's 128
+// columns as epilogue_acc32_wide_ln (when ln_part_out); C (fp32) = x' when given (never read).
+// 6 B of HBM per element instead of 10 (fp32 read + write, 16-bit hi write): the epilogue of a
+// one-round launch (proj / fc2) is HBM-bound (10 -> 8 B with a 16-bit low part: proj 85 -> 75,
+// fc2 172 -> 161 us, profiles/r05a_split_residual).
+// The wave's 80 x 128 outputs go in NI = 10 chunks of 16 rows x 64 columns (fragment row fm,
+// column half h), whose hi rows (2 KiB) and lo rows (1 KiB) arrive by LDS-DMA AHEAD chunks ahead
+// into a 4-deep per-wave ring (the 16-B chunks XOR-swizzled by row on the source address: the
+// MFMA-layout reads are conflict-free), are read in the MFMA layout, updated in place, read back as
+// rows and leave as 128-B (hi) / 64-B (lo) row segments.  Every store is a buffer store whose masked
+// lanes (rows past M, an absent output) carry an out-of-range offset, so each chunk issues a fixed
+// number of VMEM instructions and the counted wait for a chunk's DMA is a compile-time constant.
+// AHEAD = 3 and 1 measured the same in the frame (profiles/r05b_epilogue_dma_depth; 1 = debug 1 << 27).
+// `slab`: the wave's LDS region, >= 13 KiB.
 template <typename K_, int FM, int FN, int AHEAD = 3>
 __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[FM][FN], char* slab, int lane,
                                                  int m_base, int n_base) {
   #pragma clang fp contract(off)
   static_assert(FN == 8 && AHEAD >= 1 && AHEAD <= 3, "128 columns per wave, <= 4 ring slots");
-  constexpr int NI = 2 * FM, CB = 4096;   // chunks, ring slot bytes (hi | lo)
-  // VMEM instructions a chunk issues: C (4 x 16 B per lane), part (second half only), hi + lo rows (2 + 2)
-  constexpr auto st = [](int i) constexpr { return 4 + (i & 1) + 4; };
-  // the counted wait for chunk i's DMA: younger are the DMAs of chunks i+1 .. i+AHEAD (4 pieces each)
-  // and the stores of the chunks processed since chunk i's DMA was issued
+  constexpr int NI = 2 * FM, CB = 3072, LO = 2048;   // chunks, ring slot bytes (hi | lo), lo offset
+  constexpr int PCS = 3;                              // DMA pieces per chunk: hi 2, lo 1
+  // the counted wait for chunk i's DMA: younger are the DMAs of chunks i+1 .. i+AHEAD and the
+  // stores of the chunks processed since chunk i's DMA was issued (C 4, part (second half), hi 2, lo 1)
   constexpr auto younger = [](int i) constexpr {
-    int n = 4 * ((i + AHEAD < NI - 1 ? i + AHEAD : NI - 1) - i);
-    for (int j = (i - AHEAD > 0 ? i - AHEAD : 0); j < i; ++j) n += 4 + (j & 1) + 4;
+    int n = PCS * ((i + AHEAD < NI - 1 ? i + AHEAD : NI - 1) - i);
+    for (int j = (i - AHEAD > 0 ? i - AHEAD : 0); j < i; ++j) n += 4 + (j & 1) + 3;
     return n;
   };
   const int t = lane & 15, g = lane >> 4;
@@ -1097,10 +1096,10 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // the constants, before any DMA is counted
   constexpr unsigned OOB = 0xFFFFFFF0u;   // a masked store's offset: past every extent (host: < 0xFFFFFF00)
   const u16* const hi_in = p.ln_xb_out;
-  const u16* const lo_in = p.ln_xl;
-  const unsigned row_b = (unsigned)(p.M * p.ldc * 2);              // bytes of hi / lo
+  const unsigned char* const lo_in = (const unsigned char*)p.ln_xl;
+  const unsigned row_b = (unsigned)(p.M * p.ldc * 2);              // bytes of hi (lo: half)
   const __amdgpu_buffer_rsrc_t rs_hi = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_xb_out, (short)0, (int)row_b, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_lo = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_xl, (short)0, (int)row_b, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_lo = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_xl, (short)0, (int)(row_b / 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_c = __builtin_amdgcn_make_buffer_rsrc(p.C ? p.C : (void*)p.ln_xl, (short)0,
                                                                         p.C ? (int)(2 * row_b) : 0, 0x00020000);
   const int nch = p.N / 128;
@@ -1109,8 +1108,9 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
       0x00020000);
   const uint32_t slab_lds = __builtin_amdgcn_readfirstlane(lds_addr(slab)) + 1024;
   // chunk i = (fm, h): rows fm * 16 .. + 15, columns h * 64 .. + 63 of the wave's range; ring slot
-  // i & 3: hi rows [16][128 B] then lo rows; piece pc of an array = rows pc * 8 + lane / 8, 8 lanes
-  // x 16 B per 128-B row, physical 16-B chunk lane & 7 = logical chunk (lane & 7) ^ ((row >> 1) & 7)
+  // i & 3.  hi: [16][128 B], piece pc = rows pc * 8 + lane / 8, 8 lanes x 16 B per row, physical 16-B
+  // chunk lane & 7 = logical (lane & 7) ^ ((row >> 1) & 7).  lo: [16][64 B], one piece, 4 lanes x
+  // 16 B per row (row lane / 4), physical chunk lane & 3 = logical (lane & 3) ^ ((row >> 2) & 3).
   auto dma = [&](int i) __attribute__((always_inline)) {
     const int fm = i >> 1, h = i & 1;
     #pragma unroll
@@ -1119,8 +1119,11 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
       const int m = min(m_base + fm * 16 + r, p.M - 1);
       const long long o = (long long)m * p.ldc + n_base + h * 64 + (((lane & 7) ^ ((r >> 1) & 7)) << 3);
       glds16(hi_in + o, slab_lds + (i & 3) * CB + pc * 1024);
-      glds16(lo_in + o, slab_lds + (i & 3) * CB + 2048 + pc * 1024);
     }
+    const int r = lane >> 2;
+    const int m = min(m_base + fm * 16 + r, p.M - 1);
+    glds16(lo_in + (long long)m * p.ldc + n_base + h * 64 + (((lane & 3) ^ ((r >> 2) & 3)) << 4),
+           slab_lds + (i & 3) * CB + LO);
   };
   #pragma unroll
   for (int i = 0; i < AHEAD && i < NI; ++i) dma(i);
@@ -1137,17 +1140,17 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
     for (int f = 0; f < 4; ++f) {
       const int fn = h * 4 + f;
       const int off = t * 128 + (((f * 2 + (g >> 1)) ^ ((t >> 1) & 7)) << 4) + (g & 1) * 8;
+      const int loff = LO + t * 64 + ((f ^ ((t >> 2) & 3)) << 4) + g * 4;
       const uint2 hv = *(const uint2*)(buf + off);
-      const uint2 lv = *(const uint2*)(buf + 2048 + off);
-      const float xin[4] = {K_::to_f(hv.x & 0xffff) + K_::to_f(lv.x & 0xffff), K_::to_f(hv.x >> 16) + K_::to_f(lv.x >> 16),
-                            K_::to_f(hv.y & 0xffff) + K_::to_f(lv.y & 0xffff), K_::to_f(hv.y >> 16) + K_::to_f(lv.y >> 16)};
+      const uint32_t lv = *(const uint32_t*)(buf + loff);
+      const float hf[4] = {K_::to_f(hv.x & 0xffff), K_::to_f(hv.x >> 16), K_::to_f(hv.y & 0xffff), K_::to_f(hv.y >> 16)};
       const f32x4_t b = *(const f32x4_t*)(slab + (fn * 16 + 4 * g) * 4);
       const f32x4_t q = *(const f32x4_t*)(slab + 512 + (fn * 16 + 4 * g) * 4);
       f32x4_t x;
       #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = acc[fm][fn][r] + b[r];
-        x[r] = v * q[r] + xin[r];
+        x[r] = v * q[r] + lo8_decode<K_>(hf[r], unpack_i8(lv, r));
       }
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, x), rs_c,
                                              mok ? (unsigned)(((long long)m * p.ldc + n_base + fn * 16 + 4 * g) * 4)
@@ -1163,13 +1166,13 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
         s1 += d;
         s2 += d * d;
       }
-      uint2 wh, wl;
+      uint2 wh;
       wh.x = K_::pack2(x[0], x[1]);
       wh.y = K_::pack2(x[2], x[3]);
-      wl.x = K_::pack2(x[0] - K_::to_f(wh.x & 0xffff), x[1] - K_::to_f(wh.x >> 16));
-      wl.y = K_::pack2(x[2] - K_::to_f(wh.y & 0xffff), x[3] - K_::to_f(wh.y >> 16));
+      const uint32_t wl = pack_i8x4(lo8_encode<K_>(x[0], K_::to_f(wh.x & 0xffff)), lo8_encode<K_>(x[1], K_::to_f(wh.x >> 16)),
+                                    lo8_encode<K_>(x[2], K_::to_f(wh.y & 0xffff)), lo8_encode<K_>(x[3], K_::to_f(wh.y >> 16)));
       *(uint2*)(buf + off) = wh;
-      *(uint2*)(buf + 2048 + off) = wl;
+      *(uint32_t*)(buf + loff) = wl;
     }
     if (h == 1) {
       // the row's 128 columns: 4 lanes (g) of 32 values each
@@ -1188,15 +1191,19 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
       const int row = k * 8 + (lane >> 3), chunk = lane & 7;
       const int o = row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
       const uint4 dh = *(const uint4*)(buf + o);
-      const uint4 dl = *(const uint4*)(buf + 2048 + o);
       const int mm = m_base + fm * 16 + row;
       const unsigned bo = mm < p.M ? (unsigned)(((long long)mm * p.ldc + n_base + h * 64 + chunk * 8) * 2) : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{dh.x, dh.y, dh.z, dh.w}, rs_hi, bo, 0, 0);
+    }
+    {
+      const int row = lane >> 2, chunk = lane & 3;
+      const uint4 dl = *(const uint4*)(buf + LO + row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4));
+      const int mm = m_base + fm * 16 + row;
+      const unsigned bo = mm < p.M ? (unsigned)((long long)mm * p.ldc + n_base + h * 64 + chunk * 16) : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{dl.x, dl.y, dl.z, dl.w}, rs_lo, bo, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read back before this slot's next DMA
   }
-  (void)st;
 }
 
 
@@ -2481,9 +2488,9 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   }
   lds_barrier();   // the ring is free once every wave has left the K loop
   if constexpr (LNM == 3)
-    epilogue_hilo_ln<K_, FM, FN>(p, acc, smem + wave * 17408, lane, m0 + wm * TM, n0 + wn * TN);
+    epilogue_hilo_ln<K_, FM, FN>(p, acc, smem + wave * 13312, lane, m0 + wm * TM, n0 + wn * TN);
   else if constexpr (LNM == 4)
-    epilogue_hilo_ln<K_, FM, FN, 1>(p, acc, smem + wave * 17408, lane, m0 + wm * TM, n0 + wn * TN);
+    epilogue_hilo_ln<K_, FM, FN, 1>(p, acc, smem + wave * 13312, lane, m0 + wm * TM, n0 + wn * TN);
   else if constexpr (LNM == 1)
     epilogue_acc32_wide_ln<K_, FM, FN>(p, acc, smem + wave * 8192, lane, m0 + wm * TM, n0 + wn * TN);
   else if constexpr (EACT >= EPI_ACC)
@@ -2504,7 +2511,7 @@ int launch_8ph320(const GemmP& p0, hipStream_t s) {
   dim3 grid(p.tiles_n * p.tiles_m);
   if (p.ln_xl) {         // folded-LN producer on the split (hi + lo) residual stream
     if (!p.ln_xb_out || p.act != DP_ACT_NONE) return DP_ERR_ARG;
-    static_assert(8 * 17408 <= 2 * (320 * 128 + 256 * 128), "hi/lo staging fits the ring");
+    static_assert(8 * 13312 <= 2 * (320 * 128 + 256 * 128), "hi/lo staging fits the ring");
     if (p.dbg & (1 << 27)) hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 4>), grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3>), grid, dim3(512), 0, s, p);
     DP_CHECK_LAUNCH();

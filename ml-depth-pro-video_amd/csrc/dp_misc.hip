@@ -124,7 +124,7 @@ int ln_launch(const float* x, long long ldx, const LnW& lw, u16* y, long long ld
 // residual GEMMs' producer epilogue writes for the rows it makes (dp_gemm_args.ln_part_out).
 template <typename K_, int VEC>
 __global__ void __launch_bounds__(256) ln_stats_kernel(const float* __restrict__ x, long long ldx, int rows,
-                                                       u16* __restrict__ xb, long long ldxb, u16* __restrict__ xl,
+                                                       u16* __restrict__ xb, long long ldxb, int8_t* __restrict__ xl,
                                                        float* __restrict__ part) {
   constexpr int G = VEC / 2, COLS = VEC * 256, NCH = COLS / 128;
   const int lane = threadIdx.x & 63;
@@ -148,12 +148,14 @@ __global__ void __launch_bounds__(256) ln_stats_kernel(const float* __restrict__
     w.x = K_::pack2(a.x, a.y); w.y = K_::pack2(a.z, a.w);
     w.z = K_::pack2(b.x, b.y); w.w = K_::pack2(b.z, b.w);
     *(uint4*)(xb + (long long)row * ldxb + j * 512 + lane * 8) = w;
-    if (xl) {   // the split residual's low part: what the 16-bit rounding of each value dropped
-      auto lo = [](float v, uint32_t hw, int half) { return v - K_::to_f((u16)(half ? hw >> 16 : hw & 0xffff)); };
-      uint4 l;
-      l.x = K_::pack2(lo(a.x, w.x, 0), lo(a.y, w.x, 1)); l.y = K_::pack2(lo(a.z, w.y, 0), lo(a.w, w.y, 1));
-      l.z = K_::pack2(lo(b.x, w.z, 0), lo(b.y, w.z, 1)); l.w = K_::pack2(lo(b.z, w.w, 0), lo(b.w, w.w, 1));
-      *(uint4*)(xl + (long long)row * ldxb + j * 512 + lane * 8) = l;
+    if (xl) {   // the split residual's 8-bit low part: what the 16-bit rounding dropped (lo8_encode)
+      auto lo = [](float v, uint32_t hw, int half) {
+        return lo8_encode<K_>(v, K_::to_f((u16)(half ? hw >> 16 : hw & 0xffff)));
+      };
+      uint2 l;
+      l.x = pack_i8x4(lo(a.x, w.x, 0), lo(a.y, w.x, 1), lo(a.z, w.y, 0), lo(a.w, w.y, 1));
+      l.y = pack_i8x4(lo(b.x, w.z, 0), lo(b.y, w.z, 1), lo(b.z, w.w, 0), lo(b.w, w.w, 1));
+      *(uint2*)(xl + (long long)row * ldxb + j * 512 + lane * 8) = l;
     }
     if ((lane & 15) == 0) {
       const int ch = j * 4 + (lane >> 4);
@@ -541,8 +543,8 @@ extern "C" int dp_layernorm_stats(const float* x, int64_t ldx, int32_t rows, int
   dim3 grid((rows + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
 #define DP_LS(V_) do { \
-    if (dtype == DP_BF16) hipLaunchKernelGGL((ln_stats_kernel<KBF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, (u16*)xl, part); \
-    else if (dtype == DP_F16) hipLaunchKernelGGL((ln_stats_kernel<KF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, (u16*)xl, part); \
+    if (dtype == DP_BF16) hipLaunchKernelGGL((ln_stats_kernel<KBF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, (int8_t*)xl, part); \
+    else if (dtype == DP_F16) hipLaunchKernelGGL((ln_stats_kernel<KF16, V_>), grid, dim3(256), 0, s, x, (long long)ldx, rows, (u16*)xb, (long long)ldxb, (int8_t*)xl, part); \
     else return DP_ERR_DTYPE; } while (0)
   switch (cols) {
     case 512: DP_LS(2); break;

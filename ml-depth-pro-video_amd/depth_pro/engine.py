@@ -242,12 +242,13 @@ class _ViTBuffers:
         # folded LayerNorm: (mean, M2) of each 128-column chunk of the rows in `h` (un-normalised)
         self.part = torch.empty(rows, D // 128, 2, dtype=torch.float32, device=dev) if ln_fold else None
         self.h = torch.empty(rows, D, dtype=dt, device=dev)
-        # folded path: the residual stream between blocks is split, x = h + xl (16 bits each; the
-        # proj / fc2 epilogues read and update both, dp_gemm's ln_xl); `x` (fp32) holds it only where
-        # an fp32 reader needs it (the patch embed's output, the hooks, the final norm)
-        # (DP_LN_SPLIT=0, A/B only: the fp32 stream in `x`, read and written by every proj / fc2)
+        # folded path: the residual stream between blocks is split, x = h (16 bits) + an 8-bit low
+        # part xl (steps of ulp(h) / 256; the proj / fc2 epilogues read and update both, dp_gemm's
+        # ln_xl); `x` (fp32) holds it only where an fp32 reader needs it (the patch embed's output, the
+        # hooks, the final norm).  DP_LN_SPLIT=0 (A/B only): the fp32 stream in `x`, read and written
+        # by every proj / fc2
         split = ln_fold and os.environ.get("DP_LN_SPLIT", "1") == "1"
-        self.xl = torch.empty(rows, D, dtype=dt, device=dev) if split else None
+        self.xl = torch.empty(rows, D, dtype=torch.int8, device=dev) if split else None
         self.qkv = torch.empty(rows, 3 * D, dtype=dt, device=dev)
         self.a = torch.empty(rows, D, dtype=dt, device=dev)
         self.m = torch.empty(rows, MLP_DIM, dtype=dt, device=dev)

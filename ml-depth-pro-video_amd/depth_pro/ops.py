@@ -164,8 +164,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     colsum)` -- A holds un-normalised 16-bit rows with statistics `part`, B / bias are folded
     (`fold_layernorm`) and `colsum` = the row sums of B.
     Split residual (ABI 12, `ln_xl` with `ln_out=(xb, part or None)`, accumulate=True): the
-    residual stream is x = xb + ln_xl (both 16-bit), updated in place; `C` (fp32) is then only an
-    optional output of the new rows (None: not written).
+    residual stream is x = xb (16-bit) + the int8 low part ln_xl (`split_residual`), updated in place;
+    `C` (fp32) is then only an optional output of the new rows (None: not written).
     """
     if C is None:
         if ln_xl is None:
@@ -184,8 +184,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
             raise _lib.DPError("dp_gemm: ln_out buffers too small or of the wrong type")
         a.ln_xb_out, a.ln_part_out = xb.data_ptr(), _p(part)
     if ln_xl is not None:
-        if ln_out is None or ln_xl.numel() < (M - 1) * a.ldc + N or ln_xl.dtype != B.dtype:
-            raise _lib.DPError("dp_gemm: ln_xl needs ln_out and [M][ldc] 16-bit rows of the operand type")
+        if ln_out is None or ln_xl.numel() < (M - 1) * a.ldc + N or ln_xl.dtype != torch.int8:
+            raise _lib.DPError("dp_gemm: ln_xl needs ln_out and [M][ldc] int8 rows")
         a.ln_xl = ln_xl.data_ptr()
         if C.numel() == 0:
             a.C = None
@@ -315,15 +315,36 @@ def layernorm_stats(x: torch.Tensor, xb: torch.Tensor, part: torch.Tensor, rows:
                     xl: Optional[torch.Tensor] = None) -> None:
     """dp_layernorm_stats: x (fp32 rows) -> xb (16 bits) + 128-column chunk statistics `part` --
     the input side of a folded LayerNorm for rows no residual GEMM produced (ViT block 0); `xl`:
-    also the split residual's low part, x - xb in 16 bits (dp_gemm's ln_xl)."""
+    also the split residual's int8 low part (dp_gemm's ln_xl encoding, `split_residual`)."""
     if x.numel() < rows * cols or xb.numel() < rows * cols or part.numel() < rows * (cols // 128) * 2:
         raise _lib.DPError("dp_layernorm_stats: buffers smaller than rows * cols")
-    if xl is not None and (xl.numel() < rows * cols or xl.dtype != xb.dtype):
-        raise _lib.DPError("dp_layernorm_stats: xl smaller than rows * cols or not of xb's type")
+    if xl is not None and (xl.numel() < rows * cols or xl.dtype != torch.int8):
+        raise _lib.DPError("dp_layernorm_stats: xl must be int8 rows * cols")
     with _Timed("layernorm", 0.0, (rows, cols), xb.dtype):
         check(_lib.load().dp_layernorm_stats(x.data_ptr(), cols, rows, cols, xb.data_ptr(), cols,
                                              xl.data_ptr() if xl is not None else None, part.data_ptr(),
                                              dtype_code(xb.dtype), _stream(xb)), "dp_layernorm_stats")
+
+
+def split_residual(x: torch.Tensor, dt: torch.dtype):
+    """Host restatement of the split residual's encoding (dp_gemm ln_xl, ABI 12): hi = x in 16 bits,
+    q = clamp(rint((x - hi) 2^(S - e)), -128, 127) with e the frexp exponent of hi and S = 16 (bf16)
+    / 19 (f16).  Returns (hi, q int8); every step is exact in fp32, so this matches the kernels bit
+    for bit (tests)."""
+    s = 16 if dt == torch.bfloat16 else 19
+    hi = x.to(dt)
+    hf = hi.float()
+    e = torch.frexp(hf).exponent
+    q = torch.round(torch.ldexp(x.float() - hf, (s - e).float())).clamp(-128, 127).to(torch.int8)
+    return hi, q
+
+
+def merge_residual(hi: torch.Tensor, q: torch.Tensor) -> torch.Tensor:
+    """x = hi + q 2^(e - S) in fp32 (the inverse of `split_residual`, exact)."""
+    s = 16 if hi.dtype == torch.bfloat16 else 19
+    hf = hi.float()
+    e = torch.frexp(hf).exponent
+    return hf + torch.ldexp(q.float(), (e - s).float())
 
 
 def fold_layernorm(w: torch.Tensor, b: torch.Tensor, ln_w: torch.Tensor, ln_b: torch.Tensor, dt: torch.dtype,

@@ -1020,22 +1020,22 @@ def test_gemm_8ph320_ln_producer(cuda, dt, M, K):
 
 @pytest.mark.parametrize("dt", DTYPES)
 def test_layernorm_stats_split_residual(cuda, dt):
-    """dp_layernorm_stats with xl (ABI 12): xb == x in 16 bits, xl == (x - xb) in 16 bits, so that
-    xb + xl carries x to ~17 significant bits (the split residual's entry into ViT block 0)."""
+    """dp_layernorm_stats with xl (ABI 12): xb == x in 16 bits and xl == the int8 low part, exactly
+    the host restatement ops.split_residual; xb + xl carries x to ~16 significant bits (the split
+    residual's entry into ViT block 0)."""
     g = torch.Generator().manual_seed(12)
     rows = 1155
     x = torch.randn(rows, 1024, generator=g) * 3 + torch.randn(rows, 1, generator=g) * 2
+    x[0, :8] = torch.tensor([0.0, 1e-30, -1e-7, 3e-5, 65000.0, -2.0, 0.5, 1.0 + 2 ** -9])   # edges
     xb = torch.empty(rows, 1024, dtype=dt, device=cuda)
-    xl = torch.empty(rows, 1024, dtype=dt, device=cuda)
+    xl = torch.empty(rows, 1024, dtype=torch.int8, device=cuda)
     part = torch.empty(rows, 8, 2, device=cuda)
     ops.layernorm_stats(x.to(cuda), xb, part, rows, 1024, xl=xl)
-    hi = x.to(dt)
+    hi, q = ops.split_residual(x, dt)
     assert torch.equal(xb.cpu(), hi)
-    assert torch.equal(xl.cpu(), (x - hi.float()).to(dt))
-    # bf16: 8 + 8 significant bits; f16: 11 + 11, but a lo below f16's normal range (x ~ 1e-3) keeps
-    # only its absolute 2^-24 grid
-    err = (xb.cpu().float() + xl.cpu().float() - x).abs()
-    bound = 2e-5 * x.abs() if dt == torch.bfloat16 else 2e-6 * x.abs() + 6e-8
+    assert torch.equal(xl.cpu(), q)
+    err = (ops.merge_residual(xb.cpu(), xl.cpu()) - x).abs()
+    bound = 4e-5 * x.abs() + (1e-36 if dt == torch.bfloat16 else 6e-8)
     assert torch.all(err <= bound), (err - bound).max().item()
     np.testing.assert_allclose(part.cpu().double().numpy(), _chunk_stats(x).numpy(), rtol=2e-5, atol=1e-4)
 
@@ -1045,9 +1045,10 @@ def test_layernorm_stats_split_residual(cuda, dt):
                                                          (20195, 4096, True, False, 0), (20195, 1024, True, True, 1 << 27)])
 def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part, dbg):
     """Folded-LN producer on the split residual (ABI 12, dp_gemm ln_xl; the ViT proj / fc2): with the
-    stream given as hi + lo, the new rows are bit-identical to the fp32 producer's on C = hi + lo
-    (same per-element operation order): C (when asked for) equal, hi == C in 16 bits, lo == (C - hi)
-    in 16 bits, part equal; rows past M untouched (M = 20195: a 35-row last tile)."""
+    stream given as (hi, int8 lo), the new rows are bit-identical to the fp32 producer's on C =
+    merge(hi, lo) (exact in fp32; same per-element operation order): C (when asked for) equal, hi ==
+    C in 16 bits, lo == the host encoding of C (ops.split_residual), part equal; rows past M untouched
+    (M = 20195: a 35-row last tile)."""
     g = torch.Generator().manual_seed(M + K + 7)
     N = 1024
     A = rnd(M, K, dt=dt, dev=cuda, gen=g)
@@ -1055,18 +1056,17 @@ def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part
     bias = torch.randn(N, generator=g).to(cuda)
     gamma = (0.1 + 0.02 * torch.randn(N, generator=g)).to(cuda)
     x = torch.randn(M, N, generator=g) * 2 + 0.5
-    hi0 = x.to(dt)
-    lo0 = (x - hi0.float()).to(dt)
-    C1 = (hi0.float() + lo0.float()).to(cuda)            # the fp32 producer's input: exactly hi + lo
+    hi0, lo0 = ops.split_residual(x, dt)
+    C1 = ops.merge_residual(hi0, lo0).to(cuda)          # the fp32 producer's input: exactly hi + lo
     xb1 = torch.empty(M, N, dtype=dt, device=cuda)
     part1 = torch.empty(M, N // 128, 2, device=cuda)
     kw = dict(M=M, N=N, K=K, bias=bias, gamma=gamma, accumulate=True)
     ops.gemm(A, B, C1, ln_out=(xb1, part1), **kw)
     # split: hi / lo with a guard row past M on each (must stay untouched)
     hi = torch.empty(M + 1, N, dtype=dt, device=cuda)
-    lo = torch.empty(M + 1, N, dtype=dt, device=cuda)
+    lo = torch.empty(M + 1, N, dtype=torch.int8, device=cuda)
     hi[:M], lo[:M] = hi0.to(cuda), lo0.to(cuda)
-    hi[M], lo[M] = 7.0, -3.0
+    hi[M], lo[M] = 7.0, -3
     part = torch.full((M, N // 128, 2), 123.0, device=cuda) if with_part else None
     C2 = torch.full((M, N), 5.0, device=cuda) if fp32_out else None
     tile, _ = ops.gemm(A, B, C2, plan_only=True, ln_out=(hi, part), ln_xl=lo, **kw)
@@ -1080,9 +1080,10 @@ def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part
         torch.cuda.synchronize()
     finally:
         _lib.load().dp_gemm_debug_flags(0)
+    c1 = C1.cpu()
     assert torch.equal(hi[:M], xb1)
-    assert torch.equal(lo[:M], (C1 - xb1.float()).to(dt))
-    assert torch.all(hi[M] == 7.0) and torch.all(lo[M] == -3.0)
+    assert torch.equal(lo[:M].cpu(), ops.split_residual(c1, dt)[1])
+    assert torch.all(hi[M] == 7.0) and torch.all(lo[M] == -3)
     if fp32_out:
         assert torch.equal(C2, C1)
     if with_part:

@@ -47,19 +47,24 @@ def run(sd, x0, dt, mode, pre="encoder.patch_encoder."):
         x = block(sd, f"{pre}blocks.{i}.", x, dt, mode)
     return F.layer_norm(x, (1024,), sd[pre + "norm.weight"], sd[pre + "norm.bias"], L.EPS)
 
-torch.set_num_threads(8)
-img = np.random.default_rng(0).integers(0, 256, (1536, 1536, 3), dtype=np.uint8)
-xin = O.transform(img)[None]
-x0, x1, x2 = O.pyramid(xin)
-wins = torch.cat((O.split(x0, 0.25), O.split(x1, 0.5), x2), dim=0)
-pick = wins[[0, 12, 34]]
-for name, sd in (("benign", synthetic_state_dict(0)), ("stressed", stressed_state_dict(0))):
-    with torch.no_grad():
-        e0 = O.vit_embed(sd, "encoder.patch_encoder.", pick)
-        ref, _ = L.run(sd, e0, torch.float32, False)
-        line = [name]
-        for mode in ("f32", "hilo", "bf16"):
-            out = run(sd, e0, torch.bfloat16, mode)
-            e = ((out - ref).abs().mean() / ref.abs().mean()).item()
-            line.append(f"{mode} {e:.4e}")
-    print(" | ".join(line), flush=True)
+def main():
+    torch.set_num_threads(8)
+    img = np.random.default_rng(0).integers(0, 256, (1536, 1536, 3), dtype=np.uint8)
+    xin = O.transform(img)[None]
+    x0, x1, x2 = O.pyramid(xin)
+    wins = torch.cat((O.split(x0, 0.25), O.split(x1, 0.5), x2), dim=0)
+    pick = wins[[0, 12, 34]]
+    for name, sd in (("benign", synthetic_state_dict(0)), ("stressed", stressed_state_dict(0))):
+        with torch.no_grad():
+            e0 = O.vit_embed(sd, "encoder.patch_encoder.", pick)
+            ref, _ = L.run(sd, e0, torch.float32, False)
+            line = [name]
+            for mode in ("f32", "hilo", "bf16"):
+                out = run(sd, e0, torch.bfloat16, mode)
+                e = ((out - ref).abs().mean() / ref.abs().mean()).item()
+                line.append(f"{mode} {e:.4e}")
+        print(" | ".join(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
