@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """proj / fc2 residual GEMMs (the folded-LN producers, M = 20195, N = 1024) with the fp32 residual
-stream vs the split (hi + lo 16-bit) one: average launch time, warm (operands re-used, the stream
+stream vs the split one (16-bit hi + int8 lo): average launch time, warm (operands re-used, the stream
 resident in the Infinity Cache) and cold (a 512 MB write between launches evicts it, as the frame's
 other kernels do)."""
 import os
@@ -37,8 +37,7 @@ def main():
     junk = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
     flush = lambda: junk.fill_(1)  # noqa: E731
     x = torch.randn(M, N, device=dev, generator=g) * 2
-    hi = x.to(dt)
-    lo = (x - hi.float()).to(dt)
+    hi, lo = ops.split_residual(x, dt)      # the 16-bit high part and the int8 low part
     part = torch.empty(M, N // 128, 2, device=dev)
     for name, K in (("proj", 1024), ("fc2", 4096)):
         A = torch.randn(M, K, device=dev, generator=g).to(dt)
