@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Per-frame kernel-time budget by phase from a rocprofv3 --kernel-trace CSV.
+
+    python tools/frame_budget.py <kernel_trace.csv> [--md out.md]
+
+Under --kernel-trace the graph's streams run one after another, so the sums are SERIAL kernel time
+per frame (frames = patchify launches); the replayed frame overlaps the side encoders and the
+decoder chains, so it is shorter.  FLOP per phase: the algorithmic work (SURVEY 8d shapes); fraction
+of the 2.5 PFLOP/s dense bf16 / f16 MFMA peak; "to 15.4 ms" = the time the phase would take at 0.5
+of peak (the north-star's 50 % roofline, 19.247 TFLOP at 65 frames/s)."""
+import argparse
+import csv
+import re
+from collections import defaultdict
+
+PEAK = 2.5e15
+GF = 1e9
+# per-frame algorithmic FLOP of the ViT phases (M = 20195 patch rows, 577 x 2 side rows, 24 blocks)
+PATCH = {"qkv": 24 * 2 * 20195 * 3072 * 1024, "proj + fc2": 24 * 2 * 20195 * 1024 * (1024 + 4096),
+         "fc1": 24 * 2 * 20195 * 4096 * 1024, "attention (patch)": 24 * 35 * 16 * 4 * 577 * 577 * 64}
+SIDE = 24 * 2 * (2 * 577 * 1024 * (3072 + 1024 + 4096 + 4096) + 16 * 4 * 577 * 577 * 64)
+TOTAL = 19.247e12
+
+
+def classify(name, wgs):
+    n = re.sub(r"\(anonymous namespace\)::", "", name)
+    if "gemm_8ph320_kernel" in n and ", 0, 2>" in n:
+        return "qkv"
+    if "gemm_8ph320_kernel" in n and ", 16, 3>" in n or "gemm_8ph320_kernel" in n and ", 16, 1>" in n:
+        return "proj + fc2"
+    if "gemm_p8ph_kernel" in n and "true>" in n and ", 2," in n:
+        return "fc1"
+    if "ln_merge_kernel" in n or "ln_stats_kernel" in n:
+        return "LN (patch: stats, merge)"
+    if "attn_kernel" in n:
+        return "attention (patch)" if wgs > 1000 else "side encoders"
+    if "gemm_big_kernel" in n and "true, false>" in n and "128, 128" in n:
+        return "side encoders"
+    if "ln_kernel<KBF16" in n:
+        return "side encoders"
+    if "gemm_cv3_kernel" in n or ("gemm_big_kernel" in n and ("512, 128" in n)):
+        return "decoder 768^2 convs + head"
+    if "gemm_p8ph_kernel" in n or "gemm_sk_kernel" in n or "gemm_big_kernel" in n or "gemm_kernel" in n \
+            or "gemm_pbig" in n:
+        return "decoder / encoder maps (other GEMMs)"
+    if n.startswith("void at::") or "rocclr" in n or "rocblas" in n or "Cijk" in n:
+        return "torch / copies (outside the engine)"
+    return "small kernels (patchify, merge, LN, epilogues)"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--md")
+    a = ap.parse_args()
+    tot = defaultdict(float)
+    frames = 0
+    for r in csv.DictReader(open(a.trace)):
+        name = r["Kernel_Name"]
+        wgs = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
+        if "patchify_kernel" in name:
+            frames += 1
+        tot[classify(name, wgs)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+    frames = max(frames, 1)
+    flop = dict(PATCH)
+    flop["side encoders"] = SIDE
+    rest = TOTAL - sum(flop.values())
+    lines = [f"frames in the trace: {frames}; serial kernel time per frame by phase", "",
+             "| phase | ms / frame | GFLOP / frame | TFLOP/s | fraction of peak | ms at 0.5 of peak | ms to lose |",
+             "|---|---:|---:|---:|---:|---:|---:|"]
+    order = ["qkv", "attention (patch)", "proj + fc2", "fc1", "LN (patch: stats, merge)", "side encoders",
+             "decoder / encoder maps (other GEMMs)", "decoder 768^2 convs + head",
+             "small kernels (patchify, merge, LN, epilogues)", "torch / copies (outside the engine)"]
+    tsum = 0.0
+    for k in order:
+        ms = tot.get(k, 0.0) / frames / 1e3
+        if not k.startswith("torch"):          # (set-up kernels of the profiled run: weight packing etc.)
+            tsum += ms
+        f = flop.get(k)
+        if f:
+            tf = f / (ms * 1e-3) / 1e12
+            half = f / (0.5 * PEAK) * 1e3
+            lines.append(f"| {k} | {ms:.3f} | {f / GF:.0f} | {tf:.0f} | {tf * 1e12 / PEAK:.3f} | {half:.3f} | "
+                         f"{max(ms - half, 0):.3f} |")
+        else:
+            lines.append(f"| {k} | {ms:.3f} | | | | | |")
+    dec = tot.get("decoder / encoder maps (other GEMMs)", 0) + tot.get("decoder 768^2 convs + head", 0)
+    dms = dec / frames / 1e3
+    lines.append(f"| (decoder + heads + encoder maps together) | {dms:.3f} | {rest / GF:.0f} | "
+                 f"{rest / (dms * 1e-3) / 1e12:.0f} | {rest / (dms * 1e-3) / PEAK:.3f} | {rest / (0.5 * PEAK) * 1e3:.3f} | "
+                 f"{max(dms - rest / (0.5 * PEAK) * 1e3, 0):.3f} |")
+    lines.append(f"| **serial sum (engine kernels)** | **{tsum:.3f}** | {TOTAL / GF:.0f} | | | {TOTAL / (0.5 * PEAK) * 1e3:.3f} | |")
+    out = "\n".join(lines)
+    print(out)
+    if a.md:
+        open(a.md, "w").write(out + "\n")
+
+
+if __name__ == "__main__":
+    main()
