@@ -469,6 +469,7 @@ class Engine:
         self._unreported: list = []       # finished bad frames owed to the next check_status
         self.last_status: Optional[FrameStatus] = None
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
+        self.dec_early = os.environ.get("DP_DEC_EARLY", "0") == "1"
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, sync=None):
@@ -606,20 +607,28 @@ class Engine:
         ops.gemm(x, w, out, M=s_in * s_in, N=4 * cout, K=cin, bias=bias, deconv=(s_in, s_in, cout),
                  C_off=C_off, ldc=cout if ldc is None else ldc)
 
-    def _resblock(self, pre: str, x, s, out, extra=None):
-        """out = x (+ extra) + conv(relu(conv(relu(x)))) at s x s x 256 (decoder.py:96-118)."""
-        t = self.dec[s]["t"]
+    def _resblock(self, pre: str, x, s, out, extra=None, t=None):
+        """out = x (+ extra) + conv(relu(conv(relu(x)))) at s x s x 256 (decoder.py:96-118); with
+        `t` given, the first conv's output is already there (_resblock_head)."""
         P = self.P
-        self._conv3(x, s, 256, P[pre + ".1.w"], t, 256, bias=P[pre + ".1.b"], relu_a=True, act=DP_ACT_RELU)
+        if t is None:
+            t = self.dec[s]["t"]
+            self._resblock_head(pre, x, s, t)
         self._conv3(t, s, 256, P[pre + ".3.w"], out, 256, bias=P[pre + ".3.b"], R1=x, R2=extra)
 
-    def _fusion(self, i: int, feats, s, x1):
-        """FeatureFusionBlock2d i at resolution s (decoder.py:121-206; output at 2s for i != 0)."""
+    def _resblock_head(self, pre: str, x, s, t):
+        """t = relu(conv(relu(x))): the first half of a ResidualBlock (decoder.py:96-118)."""
+        P = self.P
+        self._conv3(x, s, 256, P[pre + ".1.w"], t, 256, bias=P[pre + ".1.b"], relu_a=True, act=DP_ACT_RELU)
+
+    def _fusion(self, i: int, feats, s, x1, t1=None):
+        """FeatureFusionBlock2d i at resolution s (decoder.py:121-206; output at 2s for i != 0);
+        `t1`: resnet1's first conv already computed (the early fusion-0 schedule of _forward)."""
         P, d = self.P, self.dec[s]
         p = f"decoder.fusions.{i}."
         x = feats
         if x1 is not None:
-            self._resblock(p + "resnet1", x1, s, d["x"], extra=feats)
+            self._resblock(p + "resnet1", x1, s, d["x"], extra=feats, t=t1)
             x = d["x"]
         self._resblock(p + "resnet2", x, s, d["y"])
         if i != 0:
@@ -783,6 +792,14 @@ class Engine:
                 if not serial:
                     self.dec_c.wait_stream(self.side)
                 self._fov_head()
+        # DP_DEC_EARLY=1: fusion 0's resnet1 first conv (768^2, needs only enc0) on dec_a beside
+        # fusions 4..1 instead of after them (its output in dec[768]["c"], unused at 768^2)
+        early = self.dec_early and "decoder" not in _ABLATE
+        t1 = self.dec[768]["c"] if early else None
+        if early:
+            with self._on(self.dec_a, after=ev["enc0"]):
+                self._resblock_head("decoder.fusions.0.resnet1", self.enc0, 768, t1)
+                ev["r1a"] = mark(self.dec_a)
         if "decoder" not in _ABLATE:
             f = self._fusion(4, self.low, 48, None)
             for i, s in ((3, 96), (2, 192), (1, 384)):
@@ -791,7 +808,9 @@ class Engine:
                     if i == 1:
                         main.wait_event(ev["enc0"])
                 f = self._fusion(i, f, s, self.dec[s]["c"])
-            feats = self._fusion(0, f, 768, self.enc0)
+            if early and not serial:
+                main.wait_event(ev["r1a"])
+            feats = self._fusion(0, f, 768, self.enc0, t1=t1)
         else:
             feats = self.feats
         if not serial:

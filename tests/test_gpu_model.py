@@ -323,8 +323,9 @@ def ops_resize(x3, e):
     ops.resize_bilinear(x3, e.x0)
 
 
-@pytest.mark.parametrize("gate", [None, ("qkv", "proj"), ("fc2", "fc1")])
-def test_concurrent_schedule_matches_serial_schedule(model, gate):
+@pytest.mark.parametrize("gate,early", [(None, False), (None, True), (("qkv", "proj"), False),
+                                        (("fc2", "fc1"), False)])
+def test_concurrent_schedule_matches_serial_schedule(model, gate, early):
     """The multi-stream forward (image / FOV encoders beside the patch encoder, upsample chains,
     decoder projections and FOV head beside the decoder) gives bit for bit the outputs of the
     serial order (Engine.serial_side): the same kernels on the same data, only their placement
@@ -334,9 +335,10 @@ def test_concurrent_schedule_matches_serial_schedule(model, gate):
         pytest.skip("one precision mode is enough for the schedule")
     e = m.engine()
     x = transform(frame(7)).unsqueeze(0)
-    s0, graph, g0 = e.serial_side, e.graph, e.side_gate
+    s0, graph, g0, d0 = e.serial_side, e.graph, e.side_gate, e.dec_early
     try:
         e.graph = None
+        e.dec_early = early          # fusion 0's resnet1 first conv beside fusions 4..1 (DP_DEC_EARLY)
         e.serial_side = True
         c1, f1 = (t.clone() for t in m.forward(x))
         e.serial_side = False
@@ -346,4 +348,4 @@ def test_concurrent_schedule_matches_serial_schedule(model, gate):
         e.check_status(block=True)
         assert torch.equal(c1, c2) and torch.equal(f1, f2), (c1 - c2).abs().max().item()
     finally:
-        e.serial_side, e.graph, e.side_gate = s0, graph, g0
+        e.serial_side, e.graph, e.side_gate, e.dec_early = s0, graph, g0, d0

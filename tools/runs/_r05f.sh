@@ -1,0 +1,8 @@
+#!/bin/bash
+# round 5 (f): fusion 0's resnet1 first conv beside fusions 4..1 (DP_DEC_EARLY=1): schedule test, A/B
+set -eo pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r05f
+timeout -k 10 400 python -u -m pytest tests/test_gpu_model.py -x -v --timeout 300 --timeout-method thread \
+  -m gpu -k "concurrent_schedule" > gpurun_out/r05f/pytest.log 2>&1
+bash tools/ab_env.sh r05f "DP_DEC_EARLY=0" "DP_DEC_EARLY=1"
