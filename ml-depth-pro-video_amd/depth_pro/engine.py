@@ -469,7 +469,7 @@ class Engine:
         self._unreported: list = []       # finished bad frames owed to the next check_status
         self.last_status: Optional[FrameStatus] = None
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
-        self.dec_early = os.environ.get("DP_DEC_EARLY", "0") == "1"
+        self.dec_early = os.environ.get("DP_DEC_EARLY", "1") == "1"
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, sync=None):
@@ -750,6 +750,13 @@ class Engine:
         # the main stream's f2 chain -> fuse_lowres -> convs.4, in the order the decoder's
         # projections need their outputs
         ev = {}
+        # DP_DEC_EARLY=1 (default): fusion 0's resnet1 first conv (768^2; needs only enc0, its output
+        # in dec[768]["c"], unused at 768^2) on dec_c right after the lat0 chain's last deconv, beside
+        # fusion 1 (384^2) instead of after it: 48.17 / 48.19 -> 48.60 / 48.74 fps same box
+        # (profiles/r05f_dec_early/); on dec_a with the whole lat0 chain, beside fuse_lowres and
+        # fusions 4..1, it was slower (47.61 / 47.48): the small-grid fusions then wait for CUs
+        early = self.dec_early and "decoder" not in _ABLATE
+        t1 = self.dec[768]["c"] if early else None
         with self._on(self.dec_a):
             ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
             self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
@@ -788,18 +795,13 @@ class Engine:
                 self.dec_c.wait_event(ev["lat0pre"])
             self._deconv(self.t384_256, 384, 256, P[e + "upsample_latent0.3"], self.enc0, 256)
             ev["enc0"] = mark(self.dec_c)
+            if early:
+                self._resblock_head("decoder.fusions.0.resnet1", self.enc0, 768, t1)
+                ev["r1a"] = mark(self.dec_c)
             if self.use_fov and side_ok:
                 if not serial:
                     self.dec_c.wait_stream(self.side)
                 self._fov_head()
-        # DP_DEC_EARLY=1: fusion 0's resnet1 first conv (768^2, needs only enc0) on dec_a beside
-        # fusions 4..1 instead of after them (its output in dec[768]["c"], unused at 768^2)
-        early = self.dec_early and "decoder" not in _ABLATE
-        t1 = self.dec[768]["c"] if early else None
-        if early:
-            with self._on(self.dec_a, after=ev["enc0"]):
-                self._resblock_head("decoder.fusions.0.resnet1", self.enc0, 768, t1)
-                ev["r1a"] = mark(self.dec_a)
         if "decoder" not in _ABLATE:
             f = self._fusion(4, self.low, 48, None)
             for i, s in ((3, 96), (2, 192), (1, 384)):

@@ -323,8 +323,8 @@ def ops_resize(x3, e):
     ops.resize_bilinear(x3, e.x0)
 
 
-@pytest.mark.parametrize("gate,early", [(None, False), (None, True), (("qkv", "proj"), False),
-                                        (("fc2", "fc1"), False)])
+@pytest.mark.parametrize("gate,early", [(None, False), (None, True), (("qkv", "proj"), True),
+                                        (("fc2", "fc1"), True)])
 def test_concurrent_schedule_matches_serial_schedule(model, gate, early):
     """The multi-stream forward (image / FOV encoders beside the patch encoder, upsample chains,
     decoder projections and FOV head beside the decoder) gives bit for bit the outputs of the
