@@ -735,6 +735,24 @@ class Engine:
                     pending.append((i, done))
         # patch encoder; hooks after blocks 5 / 11 (encoder.py:133-144, 267-288)
         vp = self.vp
+        ev = {}
+
+        def lat0_chain():       # encoder.py:314-324, the latent-0 project / upsample (to 384^2)
+            with self._on(self.dec_a):
+                ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
+                self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
+                self._deconv(self.t192_256, 192, 256, P[e + "upsample_latent0.2"], self.t384_256, 256)
+                ev["lat0pre"] = mark(self.dec_a)
+
+        def lat1_chain():       # ... latent 1 (to enc1, 384^2)
+            with self._on(self.dec_b):
+                ops.gemm(self.lat1, P[e + "upsample_latent1.0"], self.t96_256b, M=96 * 96, N=256, K=D)
+                self._deconv(self.t96_256b, 96, 256, P[e + "upsample_latent1.1"], self.t192_256b, 256)
+                self._deconv(self.t192_256b, 192, 256, P[e + "upsample_latent1.2"], self.enc1, 256)
+                ev["enc1"] = mark(self.dec_b)
+
+        # (measured and rejected: the latent chains started at their hooks, beside the patch encoder's
+        # blocks 6..23: 47.88 / 47.76 vs 48.17 / 48.07 fps, profiles/r05g_lat_early/)
         hooks = {5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
                  11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1)}
         self._vit(["encoder.patch_encoder."], vp, NWIN, 0, hooks, sync)
@@ -749,7 +767,6 @@ class Engine:
         # project / upsample (encoder.py:314-324): the latent and f0 / f1 chains (small grids) beside
         # the main stream's f2 chain -> fuse_lowres -> convs.4, in the order the decoder's
         # projections need their outputs
-        ev = {}
         # DP_DEC_EARLY=1 (default): fusion 0's resnet1 first conv (768^2; needs only enc0, its output
         # in dec[768]["c"], unused at 768^2) on dec_c right after the lat0 chain's last deconv, beside
         # fusion 1 (384^2) instead of after it: 48.17 / 48.19 -> 48.60 / 48.74 fps same box
@@ -757,11 +774,7 @@ class Engine:
         # fusions 4..1, it was slower (47.61 / 47.48): the small-grid fusions then wait for CUs
         early = self.dec_early and "decoder" not in _ABLATE
         t1 = self.dec[768]["c"] if early else None
-        with self._on(self.dec_a):
-            ops.gemm(self.lat0, P[e + "upsample_latent0.0"], self.t96_256, M=96 * 96, N=256, K=D)
-            self._deconv(self.t96_256, 96, 256, P[e + "upsample_latent0.1"], self.t192_256, 256)
-            self._deconv(self.t192_256, 192, 256, P[e + "upsample_latent0.2"], self.t384_256, 256)
-            ev["lat0pre"] = mark(self.dec_a)
+        lat0_chain()
         with self._on(self.dec_b):
             ops.gemm(self.f1, P[e + "upsample1.0"], self.t48_1024, M=48 * 48, N=D, K=D)
             self._deconv(self.t48_1024, 48, D, P[e + "upsample1.1"], self.enc3, D)
@@ -769,10 +782,7 @@ class Engine:
             ops.gemm(self.f0, P[e + "upsample0.0"], self.t96_512, M=96 * 96, N=512, K=D)
             self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
             ev["enc2"] = mark(self.dec_b)
-            ops.gemm(self.lat1, P[e + "upsample_latent1.0"], self.t96_256b, M=96 * 96, N=256, K=D)
-            self._deconv(self.t96_256b, 96, 256, P[e + "upsample_latent1.1"], self.t192_256b, 256)
-            self._deconv(self.t192_256b, 192, 256, P[e + "upsample_latent1.2"], self.enc1, 256)
-            ev["enc1"] = mark(self.dec_b)
+        lat1_chain()
         ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
         if not serial:

@@ -338,7 +338,7 @@ def test_concurrent_schedule_matches_serial_schedule(model, gate, early):
     s0, graph, g0, d0 = e.serial_side, e.graph, e.side_gate, e.dec_early
     try:
         e.graph = None
-        e.dec_early = early          # fusion 0's resnet1 first conv beside fusions 4..1 (DP_DEC_EARLY)
+        e.dec_early = early          # fusion 0's resnet1 first conv beside fusion 1 (DP_DEC_EARLY)
         e.serial_side = True
         c1, f1 = (t.clone() for t in m.forward(x))
         e.serial_side = False
