@@ -33,7 +33,9 @@ constexpr int CV_PATCH_B = CV_PIECES * 1024;  // bytes per patch buffer
 // correction, DP_STORE_ROWS with head_corr), CV_EPI_HPS (the composed depth head's pixel-shuffle
 // + 1x1 epilogue, DP_STORE_HEAD_PS; BN 128: one output parity per wave).
 constexpr int CV_EPI_RES = 0, CV_EPI_BC = 1, CV_EPI_HPS = 2;
-template <typename K_, bool RELU, int BN, int EPI>
+// ABL (tools/gemm_bench.py --ablate, debug bits 1 / 2 / 4 on the ReLU residual conv only): 1 no
+// epilogue, 2 no LDS-DMA in the K loop, 4 no MFMAs -- timing ablations, results garbage
+template <typename K_, bool RELU, int BN, int EPI, int ABL = 0>
 __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   constexpr int FM = 8, TN = BN / 4, FN = TN / 16, QF = FN / 2;   // wave tile 128 x TN
   constexpr int NBH = BN / 128;                                  // weight halves per K step
@@ -129,6 +131,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ABL & 4) return;
     __builtin_amdgcn_s_setprio(1);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -174,13 +177,13 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
     // phase 0), waits for step t+1, then issues the second weight half.
     readA(0, pb, ky, kx); readB(0, st); readB(1, st);
-    if (np) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
+    if (np && !(ABL & 2)) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
     bar(); mma(0, 0); mma(0, 1); bar();
     readA(1, pb, ky, kx);
-    if (n2) issue_b(0, t + 2);
+    if (n2 && !(ABL & 2)) issue_b(0, t + 2);
     if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
     else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
-    if (NBH == 2 && n2) issue_b(1, t + 2);
+    if (NBH == 2 && n2 && !(ABL & 2)) issue_b(1, t + 2);
     bar(); mma(1, 0); mma(1, 1); bar();
   }
   if (wm == 0) bar();
@@ -190,6 +193,15 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   // channels per fragment column (fn * 16 + 4 (lane >> 4)).  Same operations in the same order as
   // epilogue_rows / head_ps_rows: bit-identical to the row-raster engines.
   lds_barrier();   // the ring is free once every wave has left the K loop
+  if constexpr ((ABL & 1) != 0) {   // keep the accumulators live
+    float z = 0.f;
+    #pragma unroll
+    for (int i = 0; i < FM; ++i)
+      #pragma unroll
+      for (int j = 0; j < FN; ++j) z += acc[i][j][0];
+    if (z == 1234.5f) ((float*)p.C)[tid] = z;
+    return;
+  }
   const int t = lane & 15, g = lane >> 4;
   const int nw = n0 + wn * TN;
   f32x4_t bias[FN];
@@ -337,7 +349,14 @@ int launch_cv3(const GemmP& p0, hipStream_t s) {
 #define DP_CV3(B_, E_) do { \
     if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, B_, E_>), grid, dim3(512), 0, s, p); \
     else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, B_, E_>), grid, dim3(512), 0, s, p); } while (0)
-  if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);
+  const int abl = p.dbg & 7;
+  if (epi == CV_EPI_RES && abl && p.relu_a) {
+    switch (abl) {
+#define DP_CV3A(A_) case A_: hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, A_>), grid, dim3(512), 0, s, p); break;
+      DP_CV3A(1) DP_CV3A(2) DP_CV3A(3) DP_CV3A(4) DP_CV3A(5) DP_CV3A(6) DP_CV3A(7)
+#undef DP_CV3A
+    }
+  } else if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);
   else if (epi == CV_EPI_HPS) DP_CV3(128, CV_EPI_HPS);
   else if (bn == 256) DP_CV3(256, CV_EPI_BC);
   else DP_CV3(128, CV_EPI_BC);

@@ -23,7 +23,7 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from . import ops
-from ._lib import DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DPError, load
+from ._lib import DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DP_TILE_P8PH_256x256, DPError, load
 from .spec import DEPTH, EMBED_DIM, HEADS, IMG_SIZE, MLP_DIM, TOKENS
 
 # Timing ablations for tools/frame_ablation.py only (results are wrong when set):
@@ -470,6 +470,11 @@ class Engine:
         self.last_status: Optional[FrameStatus] = None
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
         self.dec_early = os.environ.get("DP_DEC_EARLY", "1") == "1"
+        # the patch encoder's folded qkv on the persistent 8-phase engine (+ the LN merge pre-pass), as
+        # fc1: 948 tiles of 256 x 256 over 256 workgroups instead of 3 rounds of 320 x 256 tiles, each
+        # tile's epilogue under the next one's K loop: 48.41 / 48.27 -> 49.14 / 49.06 fps same box
+        # (profiles/r05i_qkv_p8ph/); DP_QKV_P8=0: the 8-phase 320 x 256 engine (A/B)
+        self.qkv_tile = DP_TILE_P8PH_256x256 if os.environ.get("DP_QKV_P8", "1") == "1" else 0
 
     # ------------------------------------------------------------------ ViT
     def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, sync=None):
@@ -567,7 +572,7 @@ class Engine:
             b = f"{pre}blocks.{i}."
             sync("qkv", i)
             ops.gemm(buf.h, P[b + "attn.qkv.fold.w"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.fold.b"],
-                     ln_in=(buf.part, P[b + "attn.qkv.fold.s"]))
+                     ln_in=(buf.part, P[b + "attn.qkv.fold.s"]), tile=self.qkv_tile if M > 4 * TOK else 0)
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
             sync("proj", i)

@@ -42,6 +42,7 @@ SHAPES = [  # (name, M, N, K, kw)
     ("conv3x3 96^2 256->256", 96 * 96, 256, 2304, {"conv": 96}),
     ("conv3x3 48^2 256->256", 48 * 48, 256, 2304, {"conv": 48}),
     # ResidualBlock second conv: ReLU prologue + residual epilogue (f16, as the decoder runs it)
+    ("rb conv 768^2", 768 * 768, 256, 2304, {"conv": 768, "rb": True}),
     ("rb conv 384^2", 384 * 384, 256, 2304, {"conv": 384, "rb": True}),
     ("rb conv 192^2", 192 * 192, 256, 2304, {"conv": 192, "rb": True}),
     ("rb conv 96^2", 96 * 96, 256, 2304, {"conv": 96, "rb": True}),
@@ -117,11 +118,11 @@ def main():
             ms = timeit(f, args.iters)
             res.append(f"{tname} {ms*1e3:8.1f}us {flop/ms/1e9:7.1f}TF")
             if args.ablate and (tname.startswith("big") or tname.startswith("8ph") or tname.startswith("p8")
-                                or tname.startswith("dual")):
+                                or tname.startswith("dual") or tname.startswith("cv3")):
                 from depth_pro import _lib
                 parts = []
                 abl = ((1, "nostore"), (2, "noload"), (3, "nostore+noload"), (4, "nomfma"), (5, "nomfma+nostore"))
-                if not tname.startswith("big"):
+                if not tname.startswith("big") and not tname.startswith("cv3"):
                     abl = abl[:1]
                 for flags, lab in abl:
                     _lib.load().dp_gemm_debug_flags(flags)
