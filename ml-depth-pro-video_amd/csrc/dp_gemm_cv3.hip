@@ -34,7 +34,12 @@ constexpr int CV_PATCH_B = CV_PIECES * 1024;  // bytes per patch buffer
 // + 1x1 epilogue, DP_STORE_HEAD_PS; BN 128: one output parity per wave).
 constexpr int CV_EPI_RES = 0, CV_EPI_BC = 1, CV_EPI_HPS = 2;
 // ABL (tools/gemm_bench.py --ablate, debug bits 1 / 2 / 4 on the ReLU residual conv only): 1 no
-// epilogue, 2 no LDS-DMA in the K loop, 4 no MFMAs -- timing ablations, results garbage
+// epilogue, 2 no LDS-DMA in the K loop, 4 no MFMAs -- timing ablations, results garbage; 8: the
+// normal kernel plus per-workgroup clock stamps into g_cv3_stamp (tools/cv3_stamps.py); 16: no
+// barriers in the K loop; 32: the A fragments' ReLU applied by the reading wave; 64: no weight
+// LDS-DMA in the K loop; 128: no patch LDS-DMA in the K loop
+constexpr int CV_STAMPS = 6, CV_STAMP_WGS = 4096;
+__device__ unsigned long long g_cv3_stamp[CV_STAMP_WGS * CV_STAMPS];
 template <typename K_, bool RELU, int BN, int EPI, int ABL = 0>
 __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   constexpr int FM = 8, TN = BN / 4, FN = TN / 16, QF = FN / 2;   // wave tile 128 x TN
@@ -47,6 +52,8 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6;
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  unsigned long long st_[CV_STAMPS] = {};
+  if constexpr ((ABL & 8) != 0) { st_[0] = __builtin_amdgcn_s_memtime(); st_[4] = __builtin_amdgcn_s_memrealtime(); }
   const int wm = wave >> 2, wn = wave & 3;
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -118,6 +125,13 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
         const int P = (wm * 8 + qm * 4 + fm + ky) * CV_P + frow + kx;
         af[ks][fm] = *(const uint4*)(pa + P * 128 + (((ks * 4 + fchunk) ^ (P & 7)) << 4));
       }
+    if constexpr (RELU && (ABL & 32)) {   // the ReLU prologue by the reading wave, before the barrier
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        #pragma unroll
+        for (int fm = 0; fm < 4; ++fm) af[ks][fm] = relu_pk16(af[ks][fm]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
   auto readB = [&](int qn, int st) {   // columns wn*TN + qn*TN/2 .. of the tile
     const int c0 = wn * TN + qn * (TN / 2);
@@ -138,14 +152,16 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
       #pragma unroll
       for (int fm = 0; fm < 4; ++fm) {
         uint4 a = af[ks][fm];
-        if constexpr (RELU) a = relu_pk16(a);
+        if constexpr (RELU && !(ABL & 32)) a = relu_pk16(a);
         #pragma unroll
         for (int fn = 0; fn < QF; ++fn)
           acc[qm * 4 + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * QF + fn]);
       }
     __builtin_amdgcn_s_setprio(0);
   };
-  auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
+  auto bar = [&]() {
+    if constexpr ((ABL & 16) == 0) asm volatile("s_barrier" ::: "memory");
+  };
 
   // K loop: per K step (channel block cb, tap) two half-step phases {fragment reads, LDS-DMA,
   // s_barrier, MFMAs, s_barrier}; wave rows staggered by a barrier; weight step t+2 streamed in
@@ -163,6 +179,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     wait_vmcnt<0>();
   }
   lds_barrier();
+  if constexpr ((ABL & 8) != 0) st_[1] = __builtin_amdgcn_s_memtime();
   if (wm == 1) bar();
   for (int t = 0; t < KT; ++t) {
     const int cb = t / 9, tap = t - cb * 9, ky = tap / 3, kx = tap - ky * 3;
@@ -177,13 +194,13 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
     // phase 0), waits for step t+1, then issues the second weight half.
     readA(0, pb, ky, kx); readB(0, st); readB(1, st);
-    if (np && !(ABL & 2)) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
+    if (np && !(ABL & 2) && !(ABL & 128)) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
     bar(); mma(0, 0); mma(0, 1); bar();
     readA(1, pb, ky, kx);
-    if (n2 && !(ABL & 2)) issue_b(0, t + 2);
+    if (n2 && !(ABL & 2) && !(ABL & 64)) issue_b(0, t + 2);
     if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
     else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
-    if (NBH == 2 && n2 && !(ABL & 2)) issue_b(1, t + 2);
+    if (NBH == 2 && n2 && !(ABL & 2) && !(ABL & 64)) issue_b(1, t + 2);
     bar(); mma(1, 0); mma(1, 1); bar();
   }
   if (wm == 0) bar();
@@ -193,6 +210,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   // channels per fragment column (fn * 16 + 4 (lane >> 4)).  Same operations in the same order as
   // epilogue_rows / head_ps_rows: bit-identical to the row-raster engines.
   lds_barrier();   // the ring is free once every wave has left the K loop
+  if constexpr ((ABL & 8) != 0) st_[2] = __builtin_amdgcn_s_memtime();
   if constexpr ((ABL & 1) != 0) {   // keep the accumulators live
     float z = 0.f;
     #pragma unroll
@@ -319,6 +337,15 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
       for (int fn = 0; fn < FN; ++fn) { r1c[fn] = r1n[fn]; r2c[fn] = r2n[fn]; }
     }
   }
+  if constexpr ((ABL & 8) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st_[3] = __builtin_amdgcn_s_memtime();
+    st_[5] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0 && blockIdx.x < CV_STAMP_WGS) {
+      #pragma unroll
+      for (int k = 0; k < CV_STAMPS; ++k) g_cv3_stamp[blockIdx.x * CV_STAMPS + k] = st_[k];
+    }
+  }
 }
 
 template <typename K_>
@@ -349,11 +376,13 @@ int launch_cv3(const GemmP& p0, hipStream_t s) {
 #define DP_CV3(B_, E_) do { \
     if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, B_, E_>), grid, dim3(512), 0, s, p); \
     else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, B_, E_>), grid, dim3(512), 0, s, p); } while (0)
-  const int abl = p.dbg & 7;
+  const int abl = p.dbg & 255;
   if (epi == CV_EPI_RES && abl && p.relu_a) {
     switch (abl) {
 #define DP_CV3A(A_) case A_: hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, A_>), grid, dim3(512), 0, s, p); break;
-      DP_CV3A(1) DP_CV3A(2) DP_CV3A(3) DP_CV3A(4) DP_CV3A(5) DP_CV3A(6) DP_CV3A(7)
+      DP_CV3A(1) DP_CV3A(2) DP_CV3A(3) DP_CV3A(4) DP_CV3A(5) DP_CV3A(6) DP_CV3A(7) DP_CV3A(8)
+      DP_CV3A(10) DP_CV3A(12) DP_CV3A(14) DP_CV3A(24) DP_CV3A(26) DP_CV3A(28) DP_CV3A(30) DP_CV3A(40) DP_CV3A(72)
+      DP_CV3A(136)
 #undef DP_CV3A
     }
   } else if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);
@@ -366,6 +395,12 @@ int launch_cv3(const GemmP& p0, hipStream_t s) {
 }
 
 }  // namespace
+
+// debug: copy the clock stamps of the last ABL-8 launch (CV_STAMPS per workgroup) to host memory
+extern "C" int dp_cv3_stamps(unsigned long long* dst, int n_wg) {
+  if (n_wg > CV_STAMP_WGS) n_wg = CV_STAMP_WGS;
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_cv3_stamp), (size_t)n_wg * CV_STAMPS * 8, 0, hipMemcpyDeviceToHost);
+}
 
 namespace dpg {
 int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s) {
