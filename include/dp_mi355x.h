@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 12
+#define DP_ABI_VERSION 13
 int dp_abi_version(void);
 
 /*
@@ -149,6 +149,14 @@ typedef struct dp_gemm_args {
   const float* ln_colsum;
   float ln_eps;
   void* ln_xl;
+  /* ABI 13: the row statistics merged by the producer (the persistent consumer's merge pre-pass
+   * folded into the split-residual producer): with ln_rs_out set (split producer, N == 1024,
+   * ln_part_out set, a workspace), the last workgroup to finish each row tile merges the tile's
+   * rows' 8 chunk statistics into ln_rs_out[m] = (rstd, -rstd * mean) (eps ln_eps; the arithmetic
+   * of the pre-pass, bit for bit); a consumer on the persistent 8-phase engine takes ln_rs_in =
+   * that array instead of ln_part_in (no pre-pass launch, no workspace needed). */
+  float* ln_rs_out;
+  const float* ln_rs_in;
 } dp_gemm_args;
 
 enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32 = 3,

@@ -109,7 +109,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // folded LayerNorm (ln_*): the 8-phase 320 x 256 engine only, producer = the fp32 residual
   // accumulate without activation (N % 128 == 0), consumer = 16-bit C over K = 1024 rows whose
   // gamma is folded into B / bias
-  const bool lnp = a->ln_part_out || a->ln_xb_out || a->ln_xl, lnc = a->ln_part_in || a->ln_colsum;
+  const bool lnp = a->ln_part_out || a->ln_xb_out || a->ln_xl || a->ln_rs_out,
+             lnc = a->ln_part_in || a->ln_colsum || a->ln_rs_in;
   if (lnp && lnc) return DP_ERR_ARG;
   if (lnp && !a->ln_xl && (!a->ln_part_out || !a->ln_xb_out || !a->accumulate || !a->C || a->c_dtype != DP_F32 ||
                            a->act != DP_ACT_NONE || a->N % 128 != 0))
@@ -119,9 +120,18 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   if (a->ln_xl && (!a->ln_xb_out || !a->accumulate || a->c_dtype != DP_F32 || a->act != DP_ACT_NONE ||
                    a->N % 128 != 0 || a->ldc % 8 != 0 || (long long)a->M * a->ldc * 4 >= 0xFFFFFF00LL))
     return DP_ERR_ARG;
-  if (lnc && (!a->ln_part_in || !a->ln_colsum || a->K != 1024 || a->accumulate || a->c_dtype == DP_F32 ||
-              a->gamma || (a->act != DP_ACT_NONE && a->act != DP_ACT_GELU) || !(a->ln_eps > 0.f)))
+  if (lnc && (!(a->ln_part_in || a->ln_rs_in) || (a->ln_part_in && a->ln_rs_in) || !a->ln_colsum || a->K != 1024 ||
+              a->accumulate || a->c_dtype == DP_F32 || a->gamma || (a->act != DP_ACT_NONE && a->act != DP_ACT_GELU) ||
+              !(a->ln_eps > 0.f)))
     return DP_ERR_ARG;
+  // ABI 13: the producer-merged row statistics -- the split producer (8 chunks per row) with a
+  // workspace for its row-tile counters; the consumer only on the persistent engine (the 320 x 256
+  // consumer merges the chunks itself)
+  if (a->ln_rs_out && (!a->ln_xl || !a->ln_part_out || a->N != 1024 || !(a->ln_eps > 0.f) ||
+                       !(a->workspace && a->workspace_bytes >= dp_gemm_workspace_size()) ||
+                       (a->M + 319) / 320 > 1023 - LN_CNT_WORD))
+    return DP_ERR_ARG;
+  if (a->ln_rs_in && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_P8PH_256x256) return DP_ERR_ARG;
   if ((lnp || lnc) && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_8PH_320x256 &&
       !(lnc && a->tile == DP_TILE_P8PH_256x256))   // (a consumer may ask for the persistent engine)
     return DP_ERR_ARG;
@@ -281,8 +291,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // the engines with the folded-LN epilogues: the 8-phase 320 x 256 one (producer and consumer),
   // and for a consumer the planner put on the persistent 8-phase engine (the ViT fc1) that one,
   // given a workspace for its merged row statistics (debug 1 << 25: the 320 x 256 engine)
-  const bool lnc_p8 = lnc && tile == DP_TILE_P8PH_256x256 && ws_ok && !(dbg & (1 << 25)) &&
-                      (long long)(a->M + 255) / 256 * 256 * 8 <= (long long)SK_TILE_F * 4;
+  const bool lnc_p8 = lnc && tile == DP_TILE_P8PH_256x256 && (ws_ok || a->ln_rs_in) && !(dbg & (1 << 25)) &&
+                      (a->ln_rs_in || (long long)(a->M + 255) / 256 * 256 * 8 <= (long long)SK_TILE_F * 4);
+  if (a->ln_rs_in && !lnc_p8) return DP_ERR_ARG;
   if ((lnp || lnc) && !lnc_p8) tile = DP_TILE_8PH_320x256;
   if (tile == DP_TILE_8PH_320x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_BIG_320x256 && !(dbg & (1 << 15)))) {
     const bool plain = a->a_mode == DP_A_DENSE && !a->relu_a && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
@@ -323,7 +334,9 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.head_w = a->head_w; p.head_b = a->head_b; p.head_corr = a->head_corr;
   p.ln_part_out = a->ln_part_out; p.ln_xb_out = (u16*)a->ln_xb_out; p.ln_xl = (u16*)a->ln_xl;
   p.ln_part_in = a->ln_part_in; p.ln_colsum = a->ln_colsum; p.ln_eps = a->ln_eps;
-  p.ln_rs = nullptr;
+  p.ln_rs = a->ln_rs_in;
+  p.ln_rs_out = a->ln_rs_out;
+  p.ln_cnt = a->ln_rs_out ? (unsigned*)a->workspace + LN_CNT_WORD : nullptr;
   p.tiles_n = 1;
   p.tiles_m = 1;
   if (tile == DP_TILE_STREAMK_256x256) {
@@ -377,7 +390,7 @@ extern "C" int dp_gemm(const dp_gemm_args* a, dp_stream_t stream) {
   const bool conv = a->a_mode == DP_A_CONV;
   if (tile == DP_TILE_STREAMK_256x256) return launch_part_sk(p, conv, a->workspace, a->dtype == DP_BF16, s);
   if (tile == DP_TILE_SPLITK_256x256) return launch_part_splitk(p, conv, a->dtype == DP_BF16, s);
-  if (tile == DP_TILE_P8PH_256x256 && a->ln_part_in) {
+  if (tile == DP_TILE_P8PH_256x256 && a->ln_part_in && !a->ln_rs_in) {
     // folded-LN consumer on the persistent engine: merge each row's chunk statistics into
     // (rstd, -rstd * mean) in the workspace's first partial-tile slot (no stream-K launch uses
     // it meanwhile: the workspace belongs to this stream), read by the epilogue via LDS
@@ -412,6 +425,7 @@ extern "C" int dp_gemm_grouped(const dp_gemm_args* a, int32_t groups, dp_stream_
         y.accumulate != x.accumulate || y.store_mode != DP_STORE_ROWS || x.store_mode != DP_STORE_ROWS ||
         y.row_group != x.row_group || y.row_group_out != x.row_group_out || y.row_off != x.row_off ||
         y.head_w || y.head_corr || y.N % 8 != 0 || y.ln_part_out || y.ln_xb_out || y.ln_xl || y.ln_part_in ||
+        y.ln_rs_out || y.ln_rs_in ||
         y.ln_colsum)
       return DP_ERR_ARG;
     if (g == 0) p = q;

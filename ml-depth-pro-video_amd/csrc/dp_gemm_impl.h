@@ -79,7 +79,10 @@ struct GemmP {
   const float* ln_colsum;  // consumer: sum_k B[n][k]
   float ln_eps;
   const float* ln_rs;      // consumer on the persistent 8-phase engine: per row (rstd, -rstd * mean),
-                           // merged from ln_part_in by ln_merge_kernel into the GEMM workspace
+                           // merged from ln_part_in by ln_merge_kernel into the GEMM workspace, or
+                           // the producer's ln_rs_out (ABI 13)
+  float* ln_rs_out;        // split producer: the last workgroup of each row tile merges its rows
+  unsigned* ln_cnt;        // ... counting the tile's arrivals here (workspace words LN_CNT_WORD ..)
   // dp_gemm_grouped: `groups` problems of one shape in one launch (workgroup range g * tiles_m *
   // tiles_n ... covers problem g, whose operand pointers are grp[g]); 1 otherwise
   int groups;
@@ -1183,7 +1186,8 @@ __device__ __forceinline__ void epilogue_hilo_ln(const GemmP& p, f32x4_t (&acc)[
       const float mc = sh + s1 * (1.f / 128);
       const float m2 = s2 - s1 * (s1 * (1.f / 128));
       const unsigned po = (g == 0 && mok) ? (unsigned)(((long long)m * nch + n_base / 128) * 8) : OOB;
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(mc), __float_as_uint(m2)}, rs_pt, po, 0, 0);
+      // sc1 (write-through): another workgroup of the row tile may merge it (ln_merge_last)
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{__float_as_uint(mc), __float_as_uint(m2)}, rs_pt, po, 0, 16);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's staging writes
     #pragma unroll
@@ -2281,6 +2285,50 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   if (wm == 0) bar();
 }
 
+// (rstd, -rstd * mean) of a row from its 8 chunk statistics (K = 1024; Chan's merge, as
+// epilogue_mfma_lnc): ln_merge_kernel and ln_merge_last, the same arithmetic
+__device__ __forceinline__ float2 ln_merge_row(const f32x4_t (&c)[4], float eps) {
+  const float mean = (((c[0][0] + c[0][2]) + (c[1][0] + c[1][2])) + ((c[2][0] + c[2][2]) + (c[3][0] + c[3][2]))) *
+                     (1.f / 8);
+  float m2 = 0.f;
+  #pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float d0 = c[i][0] - mean, d1 = c[i][2] - mean;
+    m2 += (c[i][1] + 128.f * d0 * d0) + (c[i][3] + 128.f * d1 * d1);
+  }
+  const float rs = rsqrtf(m2 * (1.f / 1024) + eps);
+  return make_float2(rs, -rs * mean);
+}
+
+// The split producer's row merge (ABI 13, p.ln_rs_out): after its epilogue every workgroup of a
+// row tile adds one to the tile's counter; the last of the tiles_n arrivals merges the tile's rows
+// from ln_part_out (stored write-through, sc1, and drained before the add; read back with sc1
+// loads) into ln_rs_out and resets the counter for the next launch.  Replaces the persistent
+// consumer's pre-pass launch (ln_merge_kernel).  Guideline 16's sc1 hand-off: no fences.
+__device__ __forceinline__ void ln_merge_last(const GemmP& p, int tile_m, int rows, char* smem, int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's part stores (sc1) have landed
+  __syncthreads();
+  int* last = (int*)smem;
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(p.ln_cnt + tile_m, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last = old == (unsigned)(p.tiles_n - 1);
+  }
+  __syncthreads();
+  if (!*last) return;
+  if (tid == 0) __hip_atomic_store(p.ln_cnt + tile_m, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const __amdgpu_buffer_rsrc_t rs_pt = __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_part_out, (short)0,
+                                                                         (int)(p.M * 64), 0x00020000);
+  for (int r = tid; r < rows; r += blockDim.x) {
+    const int m = tile_m * rows + r;
+    if (m >= p.M) break;
+    f32x4_t c[4];
+    #pragma unroll
+    for (int i = 0; i < 4; ++i)
+      c[i] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs_pt, (unsigned)(m * 64 + i * 16), 0, 16));
+    *(float2*)(p.ln_rs_out + 2LL * m) = ln_merge_row(c, p.ln_eps);
+  }
+}
+
 // Folded LayerNorm, consumer on the persistent 8-phase engine: per row (rstd, -rstd * mean) from
 // its 8 chunk statistics (K = 1024; Chan's merge, as epilogue_mfma_lnc), one thread per row.
 __global__ void __launch_bounds__(256) ln_merge_kernel(const float* __restrict__ part, int M, float eps,
@@ -2291,16 +2339,7 @@ __global__ void __launch_bounds__(256) ln_merge_kernel(const float* __restrict__
   f32x4_t c[4];
   #pragma unroll
   for (int i = 0; i < 4; ++i) c[i] = pp[i];
-  const float mean = (((c[0][0] + c[0][2]) + (c[1][0] + c[1][2])) + ((c[2][0] + c[2][2]) + (c[3][0] + c[3][2]))) *
-                     (1.f / 8);
-  float m2 = 0.f;
-  #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float d0 = c[i][0] - mean, d1 = c[i][2] - mean;
-    m2 += (c[i][1] + 128.f * d0 * d0) + (c[i][3] + 128.f * d1 * d1);
-  }
-  const float rs = rsqrtf(m2 * (1.f / 1024) + eps);
-  *(float2*)(out + 2LL * m) = make_float2(rs, -rs * mean);
+  *(float2*)(out + 2LL * m) = ln_merge_row(c, eps);
 }
 
 template <typename K_>
@@ -2487,10 +2526,10 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
     return;
   }
   lds_barrier();   // the ring is free once every wave has left the K loop
-  if constexpr (LNM == 3)
-    epilogue_hilo_ln<K_, FM, FN>(p, acc, smem + wave * 13312, lane, m0 + wm * TM, n0 + wn * TN);
-  else if constexpr (LNM == 4)
-    epilogue_hilo_ln<K_, FM, FN, 1>(p, acc, smem + wave * 13312, lane, m0 + wm * TM, n0 + wn * TN);
+  if constexpr (LNM == 3 || LNM == 4) {
+    epilogue_hilo_ln<K_, FM, FN, LNM == 3 ? 3 : 1>(p, acc, smem + wave * 13312, lane, m0 + wm * TM, n0 + wn * TN);
+    if (p.ln_rs_out) ln_merge_last(p, tile_m, BM, smem, tid);
+  }
   else if constexpr (LNM == 1)
     epilogue_acc32_wide_ln<K_, FM, FN>(p, acc, smem + wave * 8192, lane, m0 + wm * TM, n0 + wn * TN);
   else if constexpr (EACT >= EPI_ACC)
@@ -2570,6 +2609,7 @@ constexpr int SK_RING = 2 * SK_STAGE;            // 2 stages: 128 KiB
 constexpr int SK_EPI = 8 * 16 * 64 * 4;          // 8 waves x 16 rows x 64 fp32
 constexpr int SK_TILE_F = 256 * 256;             // floats per partial slot
 constexpr long long SK_FLAG_BYTES = 4096;        // flags [0, G) (each reset by its consumer), error word at [1023] (sticky)
+constexpr int LN_CNT_WORD = 512;                 // the split producer's row-tile counters: words [512, 1023)
 static_assert(DP_GEMM_WS_ERROR_OFFSET == 4 * 1023, "error word offset (dp_mi355x.h)");
 constexpr int SK_MAX_WG = 256;
 

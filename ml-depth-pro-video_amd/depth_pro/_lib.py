@@ -26,7 +26,7 @@ INTERP_MODES = {"bilinear": DP_INTERP_BILINEAR, "bicubic": DP_INTERP_BICUBIC}
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
  DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128,
  DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256, DP_TILE_SPLITK_256x256) = range(22)
-DP_ABI_VERSION = 12
+DP_ABI_VERSION = 13
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 
@@ -72,6 +72,7 @@ class GemmArgs(ctypes.Structure):
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("ln_part_out", ctypes.c_void_p), ("ln_xb_out", ctypes.c_void_p), ("ln_part_in", ctypes.c_void_p),
         ("ln_colsum", ctypes.c_void_p), ("ln_eps", ctypes.c_float), ("ln_xl", ctypes.c_void_p),
+        ("ln_rs_out", ctypes.c_void_p), ("ln_rs_in", ctypes.c_void_p),
     ]
 
 

@@ -249,6 +249,11 @@ class _ViTBuffers:
         # by every proj / fc2
         split = ln_fold and os.environ.get("DP_LN_SPLIT", "1") == "1"
         self.xl = torch.empty(rows, D, dtype=torch.int8, device=dev) if split else None
+        # split path (ABI 13): every row's (rstd, -rstd * mean), merged by the proj / fc2 producers'
+        # last workgroup per row tile for the qkv / fc1 consumers on the persistent engine
+        # (DP_LN_RS=0, A/B: the consumer's merge pre-pass from `part` instead)
+        self.rs = (torch.empty(rows, 2, dtype=torch.float32, device=dev)
+                   if split and os.environ.get("DP_LN_RS", "1") == "1" else None)
         self.qkv = torch.empty(rows, 3 * D, dtype=dt, device=dev)
         self.a = torch.empty(rows, D, dtype=dt, device=dev)
         self.m = torch.empty(rows, MLP_DIM, dtype=dt, device=dev)
@@ -568,20 +573,25 @@ class Engine:
         ops.layernorm_stats(buf.x, buf.h, buf.part, M, D, xl=buf.xl)
         split = buf.xl is not None
         yield
+        qkv_tile = self.qkv_tile if M > 4 * TOK else 0
+        rs = buf.rs       # producer-merged row statistics (ABI 13), for the persistent consumers
         for i in range(DEPTH):
             b = f"{pre}blocks.{i}."
             sync("qkv", i)
+            rs_q = rs if (i > 0 and qkv_tile) else None     # block 0: the stats pass wrote `part` only
             ops.gemm(buf.h, P[b + "attn.qkv.fold.w"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.fold.b"],
-                     ln_in=(buf.part, P[b + "attn.qkv.fold.s"]), tile=self.qkv_tile if M > 4 * TOK else 0)
+                     ln_in=(None if rs_q is not None else buf.part, P[b + "attn.qkv.fold.s"]), ln_rs_in=rs_q,
+                     tile=qkv_tile)
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
             sync("proj", i)
             ops.gemm(buf.a, P[b + "attn.proj.weight"], None if split else buf.x, M=M, N=D, K=D,
                      bias=P[b + "attn.proj.bias"], gamma=P[b + "ls1.gamma"], accumulate=True,
-                     ln_out=(buf.h, buf.part), ln_xl=buf.xl)
+                     ln_out=(buf.h, buf.part), ln_xl=buf.xl, ln_rs_out=rs)
             sync("fc1", i)
             ops.gemm(buf.h, P[b + "mlp.fc1.fold.w"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.fold.b"],
-                     act=DP_ACT_GELU, ln_in=(buf.part, P[b + "mlp.fc1.fold.s"]))
+                     act=DP_ACT_GELU, ln_in=(None if rs is not None else buf.part, P[b + "mlp.fc1.fold.s"]),
+                     ln_rs_in=rs)
             last = i == DEPTH - 1    # the final norm reads x itself
             # fp32 rows only where they are read: the hooks (merge_windows) and the final norm
             need_x = last or bool(hooks and i in hooks) or not split
@@ -592,7 +602,7 @@ class Engine:
                 ln_out = None if last else (buf.h, buf.part)
             ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x if need_x else None, M=M, N=D, K=MLP_DIM,
                      bias=P[b + "mlp.fc2.bias"], gamma=P[b + "ls2.gamma"], accumulate=True,
-                     ln_out=ln_out, ln_xl=buf.xl)
+                     ln_out=ln_out, ln_xl=buf.xl, ln_rs_out=None if last or not qkv_tile else rs)
             if hooks and i in hooks:
                 hooks[i]()
             if last:

@@ -153,7 +153,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
          workspace: Optional[torch.Tensor] = None,
          plan_only: bool = False, border_corr: Optional[torch.Tensor] = None,
          ln_out: Optional[tuple] = None, ln_in: Optional[tuple] = None, ln_eps: float = 1e-6,
-         ln_xl: Optional[torch.Tensor] = None):
+         ln_xl: Optional[torch.Tensor] = None, ln_rs_out: Optional[torch.Tensor] = None,
+         ln_rs_in: Optional[torch.Tensor] = None):
     """dp_gemm. `A_off`/`B_off`/`C_off` are element offsets into A / B / C (sub-views, e.g. a
     K slice of a split-K GEMM: A_off = B_off = k0 with lda / ldb the full row lengths).
 
@@ -166,6 +167,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     Split residual (ABI 12, `ln_xl` with `ln_out=(xb, part or None)`, accumulate=True): the
     residual stream is x = xb (16-bit) + the int8 low part ln_xl (`split_residual`), updated in place;
     `C` (fp32) is then only an optional output of the new rows (None: not written).
+    Producer-merged row statistics (ABI 13): `ln_rs_out` (fp32 [M][2], with the split producer's
+    `ln_out=(xb, part)`, N = 1024, eps `ln_eps`, a workspace) -- the producer's last workgroup of each
+    row tile also writes every row's (rstd, -rstd * mean); a persistent-engine consumer takes it as
+    `ln_rs_in` with `ln_in=(None, colsum)` instead of merging `part` in a pre-pass launch.
     """
     if C is None:
         if ln_xl is None:
@@ -189,11 +194,20 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
         a.ln_xl = ln_xl.data_ptr()
         if C.numel() == 0:
             a.C = None
+    if ln_rs_out is not None:
+        if ln_out is None or ln_rs_out.numel() < 2 * M or ln_rs_out.dtype != torch.float32:
+            raise _lib.DPError("dp_gemm: ln_rs_out needs ln_out and fp32 [M][2]")
+        a.ln_rs_out, a.ln_eps = ln_rs_out.data_ptr(), float(ln_eps)
     if ln_in is not None:
         part, colsum = ln_in
-        if part.numel() < M * (K // 128) * 2 or colsum.numel() < N or colsum.dtype != torch.float32:
+        if (part is None) == (ln_rs_in is None) or colsum.numel() < N or colsum.dtype != torch.float32 or \
+                (part is not None and part.numel() < M * (K // 128) * 2) or \
+                (ln_rs_in is not None and (ln_rs_in.numel() < 2 * M or ln_rs_in.dtype != torch.float32)):
             raise _lib.DPError("dp_gemm: ln_in buffers too small or of the wrong type")
-        a.ln_part_in, a.ln_colsum, a.ln_eps = part.data_ptr(), colsum.data_ptr(), float(ln_eps)
+        a.ln_part_in, a.ln_colsum, a.ln_eps = _p(part), colsum.data_ptr(), float(ln_eps)
+        a.ln_rs_in = _p(ln_rs_in)
+    elif ln_rs_in is not None:
+        raise _lib.DPError("dp_gemm: ln_rs_in needs ln_in=(None, colsum)")
     if plan_only:
         t, g = ctypes.c_int32(), ctypes.c_int32()
         check(_lib.load().dp_gemm_plan(ctypes.byref(a), ctypes.byref(t), ctypes.byref(g)), "dp_gemm_plan")

@@ -1091,6 +1091,53 @@ def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M", [20195, 577])
+def test_split_producer_merged_row_stats(cuda, dt, M):
+    """ABI 13: the split producer's last workgroup per row tile merges the tile's chunk statistics
+    into (rstd, -rstd * mean) per row (dp_gemm ln_rs_out); a persistent-engine consumer reading them
+    (ln_rs_in) is bit-identical to the one that merges `part` in its pre-pass launch.  Two producer
+    launches in a row: the row-tile counters reset themselves (the second launch's statistics are
+    right too); rows past M untouched."""
+    g = torch.Generator().manual_seed(M + 31)
+    N, K, N2 = 1024, 1024, 4096
+    A = rnd(M, K, dt=dt, dev=cuda, gen=g)
+    B = rnd(N, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    bias = torch.randn(N, generator=g).to(cuda)
+    gamma = (0.1 + 0.02 * torch.randn(N, generator=g)).to(cuda)
+    x = torch.randn(M, N, generator=g) * 2 + 0.5
+    x[:, 3] += 30.0
+    hi0, lo0 = ops.split_residual(x, dt)
+    W2 = rnd(N2, K, dt=dt, dev=cuda, gen=g, scale=K ** -0.5)
+    colsum = W2.float().sum(1).contiguous()
+    b2 = torch.randn(N2, generator=g).to(cuda)
+    ws = ops.gemm_workspace(cuda)
+    from depth_pro._lib import DP_TILE_P8PH_256x256
+
+    for rep in range(2):
+        hi, lo = hi0.to(cuda), lo0.to(cuda)
+        if rep:      # another stream state: the counters must have been reset by the first launch
+            hi, lo = (hi.float() * 0.5).to(dt), lo // 2
+        part = torch.empty(M, N // 128, 2, device=cuda)
+        rs = torch.full((M + 1, 2), 9.0, device=cuda)
+        kw = dict(M=M, N=N, K=K, bias=bias, gamma=gamma, accumulate=True, workspace=ws)
+        ops.gemm(A, B, None, ln_out=(hi, part), ln_xl=lo, ln_rs_out=rs, **kw)
+        C1 = torch.empty(M, N2, dtype=dt, device=cuda)
+        C2 = torch.empty(M, N2, dtype=dt, device=cuda)
+        kc = dict(M=M, N=N2, K=K, bias=b2, act=DP_ACT_GELU, tile=DP_TILE_P8PH_256x256, workspace=ws)
+        ops.gemm(hi, W2, C1, ln_in=(part, colsum), **kc)          # pre-pass merge (ln_merge_kernel)
+        ops.gemm(hi, W2, C2, ln_in=(None, colsum), ln_rs_in=rs, **kc)
+        torch.cuda.synchronize()
+        assert torch.equal(C1, C2), (C1.float() - C2.float()).abs().max().item()
+        assert torch.all(rs[M] == 9.0)
+        # and the statistics themselves vs fp64 from the producer's own rows (hi + lo)
+        xr = ops.merge_residual(hi.cpu(), lo.cpu()).double()
+        mean, var = xr.mean(1), xr.var(1, unbiased=False)
+        r = rs[:M].cpu().double()
+        assert torch.allclose(r[:, 0], (var + 1e-6).rsqrt(), rtol=2e-5)
+        assert torch.allclose(r[:, 1], -(var + 1e-6).rsqrt() * mean, rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("act,col_scale,engine", [(0, True, "8ph320"), (DP_ACT_GELU, False, "8ph320"),
                                                   (DP_ACT_GELU, False, "p8ph")])
 def test_gemm_8ph320_ln_consumer(cuda, dt, act, col_scale, engine):
