@@ -277,7 +277,11 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     // 16-bit rows through the wave's LDS slab (16 rows x TN), stored as whole TN * 2-byte segments
     constexpr int CH = TN / 8, RPI = 64 / CH;
     char* slab = smem + wave * (16 * TN * 2);
-    uint2 r1c[FN], r2c[FN], r1n[FN], r2n[FN];
+    // residual rows PD fragment rows ahead (the K loop's fragment registers are free here): the
+    // tile's residual reads were latency-bound one row ahead (epilogue 10.3 vs 4.1 us per tile
+    // without residuals, profiles/r05j_cv3_loop/)
+    constexpr int PD = 4;
+    uint2 rb1[PD][FN], rb2[PD][FN];
     auto loadr = [&](int fm, uint2 (&r1)[FN], uint2 (&r2)[FN]) __attribute__((always_inline)) {
       if constexpr (EPI == CV_EPI_RES) {
         const long long m = mrow(fm) + t;
@@ -293,10 +297,12 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
       x[0] += K_::to_f(r.x & 0xffff); x[1] += K_::to_f(r.x >> 16);
       x[2] += K_::to_f(r.y & 0xffff); x[3] += K_::to_f(r.y >> 16);
     };
-    loadr(0, r1c, r2c);
+    #pragma unroll
+    for (int i = 0; i < PD; ++i) loadr(i, rb1[i], rb2[i]);
     #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
-      if (fm + 1 < FM) loadr(fm + 1, r1n, r2n);
+      uint2 (&r1c)[FN] = rb1[fm % PD];
+      uint2 (&r2c)[FN] = rb2[fm % PD];
       const int y = y0 + wm * 8 + fm, x = x0 + t;
       const bool border = y == 0 || y == S - 1 || x == 0 || x == S - 1;
       #pragma unroll
@@ -333,8 +339,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
         const uint4 d = *(const uint4*)(slab + row * (TN * 2) + ((chunk ^ (row & (CH - 1))) << 4));
         *(uint4*)((u16*)p.C + (mrow(fm) + row) * p.ldc + nw + chunk * 8) = d;
       }
-      #pragma unroll
-      for (int fn = 0; fn < FN; ++fn) { r1c[fn] = r1n[fn]; r2c[fn] = r2n[fn]; }
+      if (fm + PD < FM) loadr(fm + PD, r1c, r2c);
     }
   }
   if constexpr ((ABL & 8) != 0) {

@@ -500,7 +500,10 @@ class Engine:
         for the G of them (dp_gemm_grouped / dp_layernorm_grouped, attention over G * n_img)."""
         P, M = self.P, n_img * TOK
         G = len(pres)
-        ln_on, gemm_on = "ln" not in _ABLATE, "vitgemm" not in _ABLATE
+        # ablations (A/B timing only): 'ln' / 'vitgemm' everywhere; 'sideln': the grouped side pair's
+        # LayerNorm launches only (is the side chain's latency on the frame's critical path?)
+        ln_on = "ln" not in _ABLATE and not (G > 1 and "sideln" in _ABLATE)
+        gemm_on = "vitgemm" not in _ABLATE
         sync = sync or (lambda what, i: None)
 
         def lin(A, key, C, N, K, a_rows=True, **kw):
