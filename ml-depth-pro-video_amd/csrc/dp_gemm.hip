@@ -274,7 +274,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   // 96^2 -> 192^2 29.6 -> 22, 48^2 -> 96^2 (K = 1024) 42.7 -> 36, 96^2 (N = 2048) 47.5 -> 44.6 us;
   // 48 and 36 tiles were slower (26.9 -> 34, 17.1 -> 18.3 us; profiles/r03ad_deconv_small/).
   // Debug 1 << 23: off.
-  const bool dcv = a->store_mode == DP_STORE_DECONV2X2 && !a->relu_a && !a->gamma && a->act == DP_ACT_NONE;
+  const bool dcv = a->store_mode == DP_STORE_DECONV2X2 && !a->relu_a && !a->gamma && a->act == DP_ACT_NONE &&
+                   a->dc_w >= 8;   // (the persistent engine's deconv store steps its rows 8 pixels at a time)
   if (a->tile == DP_TILE_AUTO && dcv && !(dbg & (1 << 23)) && tiles256 >= 128) tile = DP_TILE_P8PH_256x256;
   if (tile == DP_TILE_P8PH_256x256 || (a->tile == DP_TILE_AUTO && tile == DP_TILE_8PH_256x256 && !(dbg & (1 << 22)))) {
     const bool ok = a->a_mode == DP_A_DENSE && a->N % 256 == 0 && a->K >= 128 && a->c_dtype != DP_F32 &&

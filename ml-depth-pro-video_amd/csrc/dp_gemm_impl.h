@@ -2021,6 +2021,21 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
       rst[fm] = *(const float2*)(rstat + (r >> 5) * 2048 + (r & 31) * 8);
     }
   }
+  // DP_STORE_DECONV2X2: a lane's 8 columns are one sub-pixel q and channels co..co+7 for the whole
+  // tile, and its rows advance by RPI = 8 pixels per store: (b, y, x) of its first row once per
+  // tile, then stepped (the per-store integer divisions cost the 384^2 -> 768^2 deconv 32 us of
+  // 158: the same GEMM with a row store ran 126 us, tools/gemm_bench.py)
+  int dq = 0, dco = 0, db = 0, dy = 0, dx = 0;
+  if constexpr (DCV) {
+    const int n = n_base + (lane % CH) * 8;
+    dq = n / p.dc_cout;
+    dco = n - dq * p.dc_cout;
+    const int m = m_base + lane / CH, hw = p.dc_h * p.dc_w;
+    db = m / hw;
+    const int rr = m - db * hw;
+    dy = rr / p.dc_w;
+    dx = rr - dy * p.dc_w;
+  }
   #pragma unroll
   for (int f0 = 0; f0 < FM; f0 += PF) {
     #pragma unroll
@@ -2060,17 +2075,20 @@ __device__ __forceinline__ void epilogue_mfma_buf(const GemmP& p, f32x4_t (&acc)
         if constexpr (DCV) {
           // DP_STORE_DECONV2X2 (epilogue4): row m = input pixel (b, y, x), column n = sub-pixel q,
           // channel co -> output pixel (b, 2y + q / 2, 2x + q % 2)
-          const int hw = p.dc_h * p.dc_w;
-          const int b = m / hw, rr = m - b * hw;
-          const int y = rr / p.dc_w, x = rr - y * p.dc_w;
-          const int q = n / p.dc_cout, co = n - q * p.dc_cout;
-          const long long pix = ((long long)b * 2 * p.dc_h + 2 * y + (q >> 1)) * (2 * p.dc_w) + 2 * x + (q & 1);
-          bo = (unsigned)((pix * p.ldc + co) * 2);
+          const long long pix = ((long long)db * 2 * p.dc_h + 2 * dy + (dq >> 1)) * (2 * p.dc_w) + 2 * dx + (dq & 1);
+          bo = (unsigned)((pix * p.ldc + dco) * 2);
         } else {
           bo = (unsigned)(((long long)m * p.ldc + n) * 2);
         }
       }
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{d.x, d.y, d.z, d.w}, crs, bo, 0, 0);
+      if constexpr (DCV) {   // the lane's next row: RPI = 8 pixels on (host: dc_w >= 8)
+        dx += RPI;
+        if (dx >= p.dc_w) {
+          dx -= p.dc_w;
+          if (++dy == p.dc_h) { dy = 0; ++db; }
+        }
+      }
     }
   }
 }

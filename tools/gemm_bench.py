@@ -52,6 +52,7 @@ SHAPES = [  # (name, M, N, K, kw)
     ("head conv 768^2 256->128", 768 * 768, 128, 2304, {"conv": 768}),
     ("composed head 768^2 128->4x32", 768 * 768, 128, 1152, {"conv": 768}),
     ("deconv 384->768 256ch", 384 * 384, 1024, 256, {"deconv": (384, 384, 256)}),
+    ("plain 384^2 x 1024 K256 (the deconv's GEMM, row store)", 384 * 384, 1024, 256, {}),
     ("deconv 192->384 256ch", 192 * 192, 1024, 256, {"deconv": (192, 192, 256)}),
 ]
 

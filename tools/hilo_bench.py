@@ -39,6 +39,13 @@ def main():
     x = torch.randn(M, N, device=dev, generator=g) * 2
     hi, lo = ops.split_residual(x, dt)      # the 16-bit high part and the int8 low part
     part = torch.empty(M, N // 128, 2, device=dev)
+    # the HBM floor of an epilogue that reads and writes the split stream once (3 + 3 B per element):
+    # a plain device copy of the same 62 MB
+    src = torch.empty(M * N * 3, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    for cl, fl in (("warm", None), ("cold", flush)):
+        us = timeit(lambda: dst.copy_(src), 20, fl)
+        print(f"copy {src.numel() / 1e6:.0f} MB ({cl}): {us:6.1f} us = {2 * src.numel() / us / 1e6:5.2f} TB/s", flush=True)
     for name, K in (("proj", 1024), ("fc2", 4096)):
         A = torch.randn(M, K, device=dev, generator=g).to(dt)
         B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
@@ -52,7 +59,8 @@ def main():
         res = []
         from depth_pro import _lib
         lib = _lib.load()
-        for lab, fn, dbg in (("fp32", f32, 0), ("split", spl, 0), ("split-ahead1", spl, 1 << 27)):
+        for lab, fn, dbg in (("fp32", f32, 0), ("split", spl, 0), ("split-ahead1", spl, 1 << 27),
+                             ("no-epilogue", spl, 1)):
             lib.dp_gemm_debug_flags(dbg)
             for cl, fl in (("warm", None), ("cold", flush)):
                 us = timeit(fn, 20, fl)
