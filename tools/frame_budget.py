@@ -26,6 +26,8 @@ def classify(name, wgs):
     n = re.sub(r"\(anonymous namespace\)::", "", name)
     if "gemm_8ph320_kernel" in n and ", 0, 2>" in n:
         return "qkv"
+    if "gemm_p8ph_kernel" in n and "false, 0, false, false, true>" in n:   # (round 5: qkv on the persistent engine)
+        return "qkv"
     if "gemm_8ph320_kernel" in n and ", 16, 3>" in n or "gemm_8ph320_kernel" in n and ", 16, 1>" in n:
         return "proj + fc2"
     if "gemm_p8ph_kernel" in n and "true>" in n and ", 2," in n:
@@ -53,19 +55,40 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--md")
     a = ap.parse_args()
+    # frames = runs of launches from one patchify launch to the next; only frames whose launches never
+    # overlap (a serial frame: the trace serialised that replay, or an eager serial forward) are summed,
+    # so a launch's duration is its own time alone on the chip, not time spent waiting for CUs
+    rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
+                   int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))) for r in csv.DictReader(open(a.trace)))
+    groups, cur = [], None
+    for r in rows:
+        if "patchify_kernel" in r[2]:
+            cur = []
+            groups.append(cur)
+        if cur is not None:
+            cur.append(r)
     tot = defaultdict(float)
-    frames = 0
-    for r in csv.DictReader(open(a.trace)):
-        name = r["Kernel_Name"]
-        wgs = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
-        if "patchify_kernel" in name:
-            frames += 1
-        tot[classify(name, wgs)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
-    frames = max(frames, 1)
+    frames = skipped = 0
+    for g in groups:
+        end, serial = 0, True
+        for t0, t1, _, _ in g:
+            if t0 < end:
+                serial = False
+                break
+            end = max(end, t1)
+        if not serial:
+            skipped += 1
+            continue
+        frames += 1
+        for t0, t1, name, wgs in g:
+            tot[classify(name, wgs)] += (t1 - t0) * 1e-3
+    if frames == 0:
+        raise SystemExit("no serial frame in the trace (every frame's launches overlap)")
     flop = dict(PATCH)
     flop["side encoders"] = SIDE
     rest = TOTAL - sum(flop.values())
-    lines = [f"frames in the trace: {frames}; serial kernel time per frame by phase", "",
+    lines = [f"serial frames in the trace: {frames} (skipped {skipped} whose launches overlap); kernel time per "
+             f"frame by phase", "",
              "| phase | ms / frame | GFLOP / frame | TFLOP/s | fraction of peak | ms at 0.5 of peak | ms to lose |",
              "|---|---:|---:|---:|---:|---:|---:|"]
     order = ["qkv", "attention (patch)", "proj + fc2", "fc1", "LN (patch: stats, merge)", "side encoders",
@@ -77,7 +100,7 @@ def main():
         if not k.startswith("torch"):          # (set-up kernels of the profiled run: weight packing etc.)
             tsum += ms
         f = flop.get(k)
-        if f:
+        if f and ms > 0:
             tf = f / (ms * 1e-3) / 1e12
             half = f / (0.5 * PEAK) * 1e3
             lines.append(f"| {k} | {ms:.3f} | {f / GF:.0f} | {tf:.0f} | {tf * 1e12 / PEAK:.3f} | {half:.3f} | "
