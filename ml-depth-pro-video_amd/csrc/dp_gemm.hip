@@ -34,6 +34,7 @@ int launch_tile(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s) {
     case DP_TILE_8PH_256x256: case DP_TILE_P8PH_256x256: return launch_part_8ph(p, tile, conv, bf16, s);
     case DP_TILE_8PH_320x256: return launch_part_8ph320(p, conv, bf16, s);
     case DP_TILE_CV3_256x256: return launch_part_cv3(p, conv, bf16, s);
+    case DP_TILE_CV3_192x256: return launch_part_cv3(p, conv, bf16, s, 12);
     case DP_TILE_BIG_320x256: case DP_TILE_BIG_512x128: return launch_part_big320(p, tile, conv, bf16, s);
     default: return launch_part_big(p, tile, conv, bf16, s);
   }
@@ -315,6 +316,18 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       a->c_dtype != DP_F32 && !a->gamma && !a->pos && !a->accumulate && a->act != DP_ACT_GELU &&
       (long long)(a->M / 256) * (a->N / 256) >= 4LL * num_cus())   // many rounds (the 768^2 maps; 384^2: 201 vs 185 us)
     tile = DP_TILE_CV3_256x256;
+  // ... and on 12 x 16-pixel tiles where those make whole rounds of workgroups and 16 x 16 ones do not
+  // (the 384^2 maps: 768 tiles = 3 rounds instead of 576 = 2.25; debug 1 << 30: off)
+  else if (a->tile == DP_TILE_AUTO && !(dbg & (1 << 16)) && !(dbg & (1 << 30)) && a->a_mode == DP_A_CONV &&
+           a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->in_w &&
+           a->out_h == a->in_h && a->out_w == a->in_w && a->in_w % 16 == 0 && a->in_w % 12 == 0 &&
+           a->in_c % 64 == 0 && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS && !a->row_group && !a->head_w &&
+           !a->head_corr && (long long)a->M * a->in_c < (1LL << 31) && off32 && a->c_dtype != DP_F32 && !a->gamma &&
+           !a->pos && !a->accumulate && a->act != DP_ACT_GELU) {
+    const long long t12 = (long long)(a->M / ((long long)a->in_w * a->in_w)) * (a->in_w / 12) * (a->in_w / 16) * (a->N / 256);
+    const long long ncu = num_cus();
+    if (t12 >= 2 * ncu && t12 % ncu == 0 && ((long long)(a->M / 256) * (a->N / 256)) % ncu != 0) tile = DP_TILE_CV3_192x256;
+  }
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
   // the border-corrected composed conv exists in the 512 x 128 conv engine only
   if (a->store_mode == DP_STORE_ROWS && a->head_corr && tile != DP_TILE_BIG_512x128 && tile != DP_TILE_CV3_256x256)
@@ -371,6 +384,7 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
     case DP_TILE_BIG_512x128: bm = 512; bn = 128; break;
     case DP_TILE_DUAL_256x128: bn = 128; break;
     case DP_TILE_PBIG_320x256: case DP_TILE_8PH_320x256: bm = 320; bn = 256; break;
+    case DP_TILE_CV3_192x256: bm = 192; bn = 256; break;
     default: bn = 256;
   }
   if (tile_out) *tile_out = tile;

@@ -22,11 +22,17 @@
 
 namespace {
 
-constexpr int CV_T = 16;                      // output tile side (pixels)
-constexpr int CV_P = CV_T + 2;                // patch side
-constexpr int CV_PIX = CV_P * CV_P;           // 324 patch pixels
-constexpr int CV_PIECES = 48;                 // 6 per wave; pieces 41-47 only hold zero-page reads
-constexpr int CV_PATCH_B = CV_PIECES * 1024;  // bytes per patch buffer
+// Output tiles of TH x 16 pixels: TH = 16 (the 768^2 maps: 2304 tiles = 9 rounds of 256 CUs) or
+// TH = 12 (DP_TILE_CV3_192x256, the 384^2 maps: 768 tiles = 3 rounds exactly, where 16 x 16 tiles
+// make 2.25 rounds); the patch is (TH + 2) x 18 pixels.
+constexpr int CV_TW = 16;                     // output tile width (pixels)
+constexpr int CV_PW = CV_TW + 2;              // patch width
+template <int TH> struct CvGeo {
+  static constexpr int PIX = (TH + 2) * CV_PW;              // patch pixels (324 / 252)
+  static constexpr int PPW = (PIX * 8 + 511) / 512;          // LDS-DMA pieces per wave (6 / 4)
+  static constexpr int PATCH_B = 8 * PPW * 1024;             // bytes per patch buffer
+  static constexpr int FM = TH / 2, HQ = FM / 2;             // fragment rows per wave / per phase
+};
 
 // BN: output channels per tile (256: the ResidualBlock convs; 128: the head convs).  EPI:
 // CV_EPI_RES (bias, ReLU, residuals; BN 256), CV_EPI_BC (bias + the composed conv's border-tap
@@ -40,9 +46,12 @@ constexpr int CV_EPI_RES = 0, CV_EPI_BC = 1, CV_EPI_HPS = 2;
 // LDS-DMA in the K loop; 128: no patch LDS-DMA in the K loop
 constexpr int CV_STAMPS = 6, CV_STAMP_WGS = 4096;
 __device__ unsigned long long g_cv3_stamp[CV_STAMP_WGS * CV_STAMPS];
-template <typename K_, bool RELU, int BN, int EPI, int ABL = 0>
+template <typename K_, bool RELU, int BN, int EPI, int ABL = 0, int TH = 16>
 __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
-  constexpr int FM = 8, TN = BN / 4, FN = TN / 16, QF = FN / 2;   // wave tile 128 x TN
+  using G = CvGeo<TH>;
+  constexpr int FM = G::FM, HQ = G::HQ, PPW = G::PPW, CV_PATCH_B = G::PATCH_B, CV_PIX = G::PIX;
+  constexpr int TN = BN / 4, FN = TN / 16, QF = FN / 2;          // wave tile 16 FM x TN
+  static_assert(TH == 16 || TH == 12, "tile rows");
   constexpr int NBH = BN / 128;                                  // weight halves per K step
   constexpr int B_B = BN * 128;                                  // bytes per weight K step
   static_assert(EPI != CV_EPI_RES || BN == 256, "residual epilogue: BN 256");
@@ -59,23 +68,23 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   // XCD-contiguous: an XCD's workgroups are consecutive tiles of a tile row (shared halos)
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int S = p.out_w, tpr = S / CV_T, tpi = tpr * tpr;
+  const int S = p.out_w, tpr = S / CV_TW, tpi = (S / TH) * tpr;
   const int tn = wgid % p.tiles_n, sp = wgid / p.tiles_n;
   const int img = sp / tpi, r_ = sp - img * tpi;
-  const int y0 = (r_ / tpr) * CV_T, x0 = (r_ % tpr) * CV_T, n0 = tn * BN;
+  const int y0 = (r_ / tpr) * TH, x0 = (r_ % tpr) * CV_TW, n0 = tn * BN;
   const int cin = p.in_c, CB = cin / 64;
   const int KT = CB * 9;
 
   // patch pieces of this lane: element offset of its 16-B chunk (channel block 0), or -1 when
   // the pixel is in the zero padding or past the patch
-  int poff[6];
+  int poff[PPW];
   #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int c = (wave * 6 + i) * 64 + lane;   // chunk index in the patch image
+  for (int i = 0; i < PPW; ++i) {
+    const int c = (wave * PPW + i) * 64 + lane;   // chunk index in the patch image
     const int P = c >> 3, slot = c & 7;
     int off = -1;
     if (P < CV_PIX) {
-      const int pr = P / CV_P, pc = P - pr * CV_P;
+      const int pr = P / CV_PW, pc = P - pr * CV_PW;
       const int iy = y0 - 1 + pr, ix = x0 - 1 + pc;
       if ((unsigned)iy < (unsigned)S && (unsigned)ix < (unsigned)S)
         off = ((img * S + iy) * S + ix) * cin + ((slot ^ (P & 7)) << 3);
@@ -99,10 +108,10 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     #pragma unroll
     for (int i = 0; i < 2; ++i) glds16(p.B + (boff[h][i] + t * 64), dst + i * 8192);
   };
-  auto issue_patch3 = [&](int cb, int buf, int i0) {   // 3 of the wave's 6 patch pieces
-    const uint32_t dst = lds0 + buf * CV_PATCH_B + wave_u * 6 * 1024;
+  auto issue_patch3 = [&](int cb, int buf, int i0) {   // half of the wave's PPW patch pieces
+    const uint32_t dst = lds0 + buf * CV_PATCH_B + wave_u * PPW * 1024;
     #pragma unroll
-    for (int i = i0; i < i0 + 3; ++i) {
+    for (int i = i0; i < i0 + PPW / 2; ++i) {
       const void* src = poff[i] >= 0 ? (const void*)(p.A + (poff[i] + cb * 64)) : (const void*)g_zero_page;
       glds16(src, dst + i * 1024);
     }
@@ -114,22 +123,22 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int frow = lane & 15, fchunk = lane >> 4;
-  uint4 af[2][4], bf[2][2][QF];
-  // quadrant qm of the wave tile = output pixel rows wm*8 + qm*4 .. +3; tap (ky, kx) of patch buffer pb
+  uint4 af[2][HQ], bf[2][2][QF];
+  // half qm of the wave tile = output pixel rows wm*FM + qm*HQ .. +HQ-1; tap (ky, kx) of patch buffer pb
   auto readA = [&](int qm, int pb, int ky, int kx) {
     const char* pa = smem + pb * CV_PATCH_B;
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
-      for (int fm = 0; fm < 4; ++fm) {
-        const int P = (wm * 8 + qm * 4 + fm + ky) * CV_P + frow + kx;
+      for (int fm = 0; fm < HQ; ++fm) {
+        const int P = (wm * FM + qm * HQ + fm + ky) * CV_PW + frow + kx;
         af[ks][fm] = *(const uint4*)(pa + P * 128 + (((ks * 4 + fchunk) ^ (P & 7)) << 4));
       }
     if constexpr (RELU && (ABL & 32)) {   // the ReLU prologue by the reading wave, before the barrier
       #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
         #pragma unroll
-        for (int fm = 0; fm < 4; ++fm) af[ks][fm] = relu_pk16(af[ks][fm]);
+        for (int fm = 0; fm < HQ; ++fm) af[ks][fm] = relu_pk16(af[ks][fm]);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -150,12 +159,12 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
-      for (int fm = 0; fm < 4; ++fm) {
+      for (int fm = 0; fm < HQ; ++fm) {
         uint4 a = af[ks][fm];
         if constexpr (RELU && !(ABL & 32)) a = relu_pk16(a);
         #pragma unroll
         for (int fn = 0; fn < QF; ++fn)
-          acc[qm * 4 + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * QF + fn]);
+          acc[qm * HQ + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * HQ + fm][qn * QF + fn]);
       }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -168,7 +177,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   // phase 1 (its stage's reads ended in phase 0), the next block's patch in phase 0 of a block's
   // first step; one counted wait per step (phase 1) for step t+1.
   // prologue: patch of block 0 and weight steps 0 and 1
-  issue_patch3(0, 0, 0); issue_patch3(0, 0, 3);
+  issue_patch3(0, 0, 0); issue_patch3(0, 0, PPW / 2);
   #pragma unroll
   for (int h = 0; h < NBH; ++h) issue_b(h, 0);
   if (KT > 1) {
@@ -194,11 +203,11 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
     // phase 0), waits for step t+1, then issues the second weight half.
     readA(0, pb, ky, kx); readB(0, st); readB(1, st);
-    if (np && !(ABL & 2) && !(ABL & 128)) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, 3); }
+    if (np && !(ABL & 2) && !(ABL & 128)) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, PPW / 2); }
     bar(); mma(0, 0); mma(0, 1); bar();
     readA(1, pb, ky, kx);
     if (n2 && !(ABL & 2) && !(ABL & 64)) issue_b(0, t + 2);
-    if (np) { if (n2) wait_vmcnt<8>(); else wait_vmcnt<6>(); }
+    if (np) { if (n2) wait_vmcnt<PPW + 2>(); else wait_vmcnt<PPW>(); }
     else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
     if (NBH == 2 && n2 && !(ABL & 2) && !(ABL & 64)) issue_b(1, t + 2);
     bar(); mma(1, 0); mma(1, 1); bar();
@@ -206,7 +215,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   if (wm == 0) bar();
 
   // epilogues in the MFMA register layout: fragment row fm of the wave is output pixel row
-  // wm * 8 + fm of the tile (16 consecutive pixels, lane & 15), each lane 4 consecutive
+  // wm * FM + fm of the tile (16 consecutive pixels, lane & 15), each lane 4 consecutive
   // channels per fragment column (fn * 16 + 4 (lane >> 4)).  Same operations in the same order as
   // epilogue_rows / head_ps_rows: bit-identical to the row-raster engines.
   lds_barrier();   // the ring is free once every wave has left the K loop
@@ -226,7 +235,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   #pragma unroll
   for (int fn = 0; fn < FN; ++fn)
     bias[fn] = p.bias ? *(const f32x4_t*)(p.bias + nw + fn * 16 + 4 * g) : f32x4_t{0.f, 0.f, 0.f, 0.f};
-  auto mrow = [&](int fm) { return (long long)((img * S + y0 + wm * 8 + fm) * S + x0); };
+  auto mrow = [&](int fm) { return (long long)((img * S + y0 + wm * FM + fm) * S + x0); };
   if constexpr (EPI == CV_EPI_HPS) {
     // composed depth head (head_ps_rows): this wave's 32 columns are parity q = wn of output
     // channels o = fn * 16 + 4 g + r; z = acc + bias - border taps of head.2's zero padding,
@@ -240,7 +249,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     const long long W2 = 2LL * S;
     #pragma unroll 1
     for (int fm = 0; fm < FM; ++fm) {
-      const int y = y0 + wm * 8 + fm, x = x0 + t;
+      const int y = y0 + wm * FM + fm, x = x0 + t;
       float z[FN][4];
       #pragma unroll
       for (int fn = 0; fn < FN; ++fn)
@@ -303,7 +312,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     for (int fm = 0; fm < FM; ++fm) {
       uint2 (&r1c)[FN] = rb1[fm % PD];
       uint2 (&r2c)[FN] = rb2[fm % PD];
-      const int y = y0 + wm * 8 + fm, x = x0 + t;
+      const int y = y0 + wm * FM + fm, x = x0 + t;
       const bool border = y == 0 || y == S - 1 || x == 0 || x == S - 1;
       #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
@@ -354,11 +363,11 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
 }
 
 template <typename K_>
-int launch_cv3(const GemmP& p0, hipStream_t s) {
+int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
   GemmP p = p0;
   const int S = p.out_w;
   if (p.k_h != 3 || p.k_w != 3 || p.stride != 1 || p.pad != 1 || p.in_h != S || p.in_w != S || p.out_h != S ||
-      S % CV_T || p.in_c % 64 || p.M % (S * S) || p.row_group || (p.head_w && p.store_mode != DP_STORE_HEAD_PS) ||
+      S % CV_TW || S % th || p.in_c % 64 || p.M % (S * S) || p.row_group || (p.head_w && p.store_mode != DP_STORE_HEAD_PS) ||
       p.gamma || p.pos || p.accumulate || (p.act != DP_ACT_NONE && p.act != DP_ACT_RELU))
     return DP_ERR_ARG;
   if ((long long)p.M * p.in_c >= (1LL << 31) || (long long)p.N * p.ldb >= (1LL << 31)) return DP_ERR_ARG;
@@ -375,13 +384,21 @@ int launch_cv3(const GemmP& p0, hipStream_t s) {
   } else {
     return DP_ERR_ARG;
   }
+  if (th == 12 && epi != CV_EPI_RES) return DP_ERR_ARG;   // (12-row tiles: the ResidualBlock-type convs only)
   p.tiles_n = p.N / bn;
-  p.tiles_m = (p.M / (S * S)) * (S / CV_T) * (S / CV_T);
+  p.tiles_m = (p.M / (S * S)) * (S / th) * (S / CV_TW);
   dim3 grid(p.tiles_m * p.tiles_n);
+  const int abl = p.dbg & 255;
+  if (th == 12) {
+    if (abl == 8 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 8, 12>), grid, dim3(512), 0, s, p);
+    else if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 0, 12>), grid, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 256, CV_EPI_RES, 0, 12>), grid, dim3(512), 0, s, p);
+    DP_CHECK_LAUNCH();
+    return 0;
+  }
 #define DP_CV3(B_, E_) do { \
     if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, B_, E_>), grid, dim3(512), 0, s, p); \
     else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, B_, E_>), grid, dim3(512), 0, s, p); } while (0)
-  const int abl = p.dbg & 255;
   if (epi == CV_EPI_RES && abl && p.relu_a) {
     switch (abl) {
 #define DP_CV3A(A_) case A_: hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, A_>), grid, dim3(512), 0, s, p); break;
@@ -408,8 +425,8 @@ extern "C" int dp_cv3_stamps(unsigned long long* dst, int n_wg) {
 }
 
 namespace dpg {
-int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s) {
+int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s, int th) {
   if (!conv) return DP_ERR_ARG;
-  return bf16 ? launch_cv3<KBF16>(p, s) : launch_cv3<KF16>(p, s);
+  return bf16 ? launch_cv3<KBF16>(p, s, th) : launch_cv3<KF16>(p, s, th);
 }
 }  // namespace dpg

@@ -116,7 +116,7 @@ constexpr int TILE_GRP_128x128 = -1;   // internal: the grouped (side-encoder) l
 int launch_part_big320(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);   // dp_gemm_big320.hip
 int launch_part_8ph(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);      // dp_gemm_8ph.hip
 int launch_part_8ph320(const GemmP& p, bool conv, bool bf16, hipStream_t s);             // dp_gemm_8ph320.hip
-int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s);                // dp_gemm_cv3.hip
+int launch_part_cv3(const GemmP& p, bool conv, bool bf16, hipStream_t s, int th = 16);                // dp_gemm_cv3.hip
 int launch_part_pbig(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);     // dp_gemm_pbig.hip
 int launch_part_small(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s);    // dp_gemm_small.hip
 int launch_part_sk(const GemmP& p, bool conv, void* ws, bool bf16, hipStream_t s);       // dp_gemm_sk.hip

@@ -879,21 +879,29 @@ def test_8phase_320_bit_identical_to_320(cuda, dt, case):
 
 
 @pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("th", [16, 12])
 @pytest.mark.parametrize("case", ["relu_bias_relu", "residual2", "cin128_n512",
                                   "big_relu_bias_relu", "big_residual2_cin192", "big_cin128_n512"])
-def test_patch_conv3x3_bit_identical(cuda, dt, case):
+def test_patch_conv3x3_bit_identical(cuda, dt, case, th):
     """The 3x3 patch-conv engine (DP_TILE_CV3_256x256: 16 x 16 pixel tiles, the input patch of a
     channel block in LDS, the 9 taps read from it) gives exactly the 256 x 256 big engine's result
     -- same K order, same zero padding, same epilogue -- for the decoder ResidualBlock convs (ReLU
     on load + bias + ReLU; bias + two residuals), 2 images, a wider N; and matches F.conv2d.
     big_*: more tiles than CUs (576 tiles; 2 x 256 tiles with 3 channel blocks = an odd K-step count
-    per tile; 2 column tiles of 144)."""
-    from depth_pro._lib import DP_TILE_CV3_256x256
+    per tile; 2 column tiles of 144).  th = 12: the 12 x 16-pixel tiles (DP_TILE_CV3_192x256), maps
+    whose side is a multiple of 48."""
+    from depth_pro._lib import DP_TILE_CV3_192x256, DP_TILE_CV3_256x256
 
     g = torch.Generator().manual_seed(sum(map(ord, case)))
     S, Ci, Co, nb = {"relu_bias_relu": (96, 256, 256, 1), "residual2": (64, 256, 256, 2),
                      "cin128_n512": (48, 128, 512, 1), "big_relu_bias_relu": (384, 256, 256, 1),
                      "big_residual2_cin192": (256, 192, 256, 2), "big_cin128_n512": (192, 128, 512, 1)}[case]
+    if th == 12 and S % 48:
+        if case == "residual2":
+            S = 48          # the residual epilogue on 12-row tiles too
+        else:
+            pytest.skip("12-row tiles need a side divisible by 48")
+    tile = DP_TILE_CV3_256x256 if th == 16 else DP_TILE_CV3_192x256
     x = rnd(nb, Ci, S, S, dt=dt, dev=cuda, gen=g)
     w = rnd(Co, Ci, 3, 3, dt=dt, dev=cuda, gen=g, scale=(9 * Ci) ** -0.5)
     b = torch.randn(Co, generator=g).to(cuda)
@@ -911,11 +919,26 @@ def test_patch_conv3x3_bit_identical(cuda, dt, case):
         ref = ref + (r1.float() + r2.float()).reshape(nb, S, S, Co).permute(0, 3, 1, 2)
     out1 = torch.full((nb * S * S, Co), 7.0, dtype=dt, device=cuda)
     out2 = out1.clone()
-    ops.gemm(xh, ops.conv_weight(w), out1, tile=DP_TILE_CV3_256x256, **kw)
+    ops.gemm(xh, ops.conv_weight(w), out1, tile=tile, **kw)
     ops.gemm(xh, ops.conv_weight(w), out2, tile=DP_TILE_BIG_256x256, **kw)
     torch.cuda.synchronize()
     assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max().item()
-    close(out1.reshape(nb, S, S, Co).permute(0, 3, 1, 2), ref, dt, f"cv3 {case}")
+    close(out1.reshape(nb, S, S, Co).permute(0, 3, 1, 2), ref, dt, f"cv3 {case} th {th}")
+
+
+def test_patch_conv3x3_planner_tiles(cuda):
+    """The planner's patch-conv tiles for the decoder ResidualBlock shapes: 16 x 16 at 768^2 (2304
+    tiles = whole rounds), 12 x 16 at 384^2 (768 = 3 rounds; 16 x 16 would make 2.25)."""
+    from depth_pro._lib import DP_TILE_CV3_192x256, DP_TILE_CV3_256x256
+
+    A = torch.empty(8, dtype=torch.float16, device=cuda)
+    want = {768: DP_TILE_CV3_256x256}
+    if torch.cuda.get_device_properties(cuda).multi_processor_count == 256:
+        want[384] = DP_TILE_CV3_192x256
+    for S, t in want.items():
+        conv = dict(in_h=S, in_w=S, in_c=256, k=3, stride=1, pad=1, out_h=S, out_w=S)
+        tile, _ = ops.gemm(A, A, A, M=S * S, N=256, K=2304, conv=conv, relu_a=True, act=DP_ACT_RELU, plan_only=True)
+        assert tile == t, (S, tile)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

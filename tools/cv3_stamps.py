@@ -15,7 +15,7 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ml-depth-pro-video_amd"))
 from depth_pro import _lib, ops  # noqa: E402
-from depth_pro._lib import DP_TILE_CV3_256x256  # noqa: E402
+from depth_pro._lib import DP_TILE_CV3_192x256, DP_TILE_CV3_256x256  # noqa: E402
 
 
 def main():
@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--size", type=int, default=768)
     ap.add_argument("--no-res", action="store_true", help="no residual (a ResidualBlock's first conv)")
     ap.add_argument("--seconds", type=float, default=2.0)
+    ap.add_argument("--th", type=int, default=16, help="tile rows: 16 (DP_TILE_CV3_256x256) or 12 (..._192x256)")
     ap.add_argument("--abl", type=int, default=0, help="extra ablation bits with the stamps: 2 no loads, 4 no MFMA, "
                     "16 no barriers (timing only)")
     args = ap.parse_args()
@@ -40,7 +41,7 @@ def main():
 
     def run():
         ops.gemm(A, B, C, M=S * S, N=N, K=9 * cin, conv=conv, bias=bias, relu_a=True, act=0 if R1 is not None else 1,
-                 R1=R1, ldr1=N if R1 is not None else 0, tile=DP_TILE_CV3_256x256)
+                 R1=R1, ldr1=N if R1 is not None else 0, tile=DP_TILE_CV3_256x256 if args.th == 16 else DP_TILE_CV3_192x256)
 
     for flags, lab in (((0, "plain"),) if not args.abl else ()) + ((8 | args.abl, f"stamped (bits {8 | args.abl})"),):
         lib.dp_gemm_debug_flags(flags)
@@ -59,7 +60,7 @@ def main():
                 break
         print(f"{lab}: {1000 * e0.elapsed_time(e1) / n:.1f} us per launch ({n} launches)")
     lib.dp_gemm_debug_flags(0)
-    nwg = (S // 16) ** 2
+    nwg = (S // 16) * (S // args.th)
     buf = (ctypes.c_ulonglong * (nwg * 6))()
     lib.dp_cv3_stamps.restype = ctypes.c_int
     assert lib.dp_cv3_stamps(buf, nwg) == 0
@@ -74,7 +75,7 @@ def main():
                    ("workgroup", tot)):
         print(f"  {lab:36s} median {np.median(v):9.0f} cyc = {np.median(v) / mhz:7.2f} us  "
               f"(p10 {np.percentile(v, 10) / mhz:6.2f}, p90 {np.percentile(v, 90) / mhz:6.2f})")
-    print(f"  K loop per step: {np.median(loop) / kt:.0f} cyc (MFMA floor 2 waves x 64 x 16 = 2048)")
+    print(f"  K loop per step: {np.median(loop) / kt:.0f} cyc (MFMA floor 2 waves x {8 * args.th // 2} MFMAs x 16 = {128 * args.th})")
     # workgroup rounds: start-time spread
     t0 = st[:, 0] - st[:, 0].min()
     print(f"  launch span {(st[:, 3].max() - st[:, 0].min()) / mhz:.1f} us")
