@@ -317,7 +317,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
       (long long)(a->M / 256) * (a->N / 256) >= 4LL * num_cus())   // many rounds (the 768^2 maps; 384^2: 201 vs 185 us)
     tile = DP_TILE_CV3_256x256;
   // ... and on 12 x 16-pixel tiles where those make whole rounds of workgroups and 16 x 16 ones do not
-  // (the 384^2 maps: 768 tiles = 3 rounds instead of 576 = 2.25; debug 1 << 30: off)
+  // (the 384^2 maps: 768 tiles = 3 rounds instead of 576 = 2.25: 218 -> 187 us, 49.53 / 49.77 ->
+  // 50.00 / 49.99 fps same box, profiles/r05y_cv3_12row/; debug 1 << 30: off)
   else if (a->tile == DP_TILE_AUTO && !(dbg & (1 << 16)) && !(dbg & (1 << 30)) && a->a_mode == DP_A_CONV &&
            a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->in_w &&
            a->out_h == a->in_h && a->out_w == a->in_w && a->in_w % 16 == 0 && a->in_w % 12 == 0 &&
@@ -327,6 +328,10 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     const long long t12 = (long long)(a->M / ((long long)a->in_w * a->in_w)) * (a->in_w / 12) * (a->in_w / 16) * (a->N / 256);
     const long long ncu = num_cus();
     if (t12 >= 2 * ncu && t12 % ncu == 0 && ((long long)(a->M / 256) * (a->N / 256)) % ncu != 0) tile = DP_TILE_CV3_192x256;
+    // ... and single-round grids of at least half the CUs (the 192^2 convs: 192 workgroups of
+    // 192 x 256 instead of 144 of 256 x 256: 81.8 -> 62.7 us alone, 49.02 / 49.09 -> 49.39 / 49.25 fps
+    // same box, profiles/r05z_cv3_192/)
+    else if (t12 <= ncu && 2 * t12 >= ncu) tile = DP_TILE_CV3_192x256;
   }
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
   // the border-corrected composed conv exists in the 512 x 128 conv engine only

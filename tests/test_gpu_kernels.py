@@ -928,13 +928,15 @@ def test_patch_conv3x3_bit_identical(cuda, dt, case, th):
 
 def test_patch_conv3x3_planner_tiles(cuda):
     """The planner's patch-conv tiles for the decoder ResidualBlock shapes: 16 x 16 at 768^2 (2304
-    tiles = whole rounds), 12 x 16 at 384^2 (768 = 3 rounds; 16 x 16 would make 2.25)."""
+    tiles = whole rounds), 12 x 16 at 384^2 (768 = 3 rounds; 16 x 16 would make 2.25) and at 192^2
+    (one round of 192 workgroups)."""
     from depth_pro._lib import DP_TILE_CV3_192x256, DP_TILE_CV3_256x256
 
     A = torch.empty(8, dtype=torch.float16, device=cuda)
     want = {768: DP_TILE_CV3_256x256}
     if torch.cuda.get_device_properties(cuda).multi_processor_count == 256:
         want[384] = DP_TILE_CV3_192x256
+        want[192] = DP_TILE_CV3_192x256     # a single round of 192 workgroups instead of 144
     for S, t in want.items():
         conv = dict(in_h=S, in_w=S, in_c=256, k=3, stride=1, pad=1, out_h=S, out_w=S)
         tile, _ = ops.gemm(A, A, A, M=S * S, N=256, K=2304, conv=conv, relu_a=True, act=DP_ACT_RELU, plan_only=True)
