@@ -43,8 +43,10 @@ constexpr int CV_EPI_RES = 0, CV_EPI_BC = 1, CV_EPI_HPS = 2;
 // epilogue, 2 no LDS-DMA in the K loop, 4 no MFMAs -- timing ablations, results garbage; 8: the
 // normal kernel plus per-workgroup clock stamps into g_cv3_stamp (tools/cv3_stamps.py); 16: no
 // barriers in the K loop; 32: the A fragments' ReLU applied by the reading wave; 64: no weight
-// LDS-DMA in the K loop; 128: no patch LDS-DMA in the K loop
-constexpr int CV_STAMPS = 6, CV_STAMP_WGS = 4096;
+// LDS-DMA in the K loop; 128: no patch LDS-DMA in the K loop; 256 (with 8): wave 0's K-loop cycles by
+// kind into stamps 6..9
+constexpr int CV_STAMPS = 10, CV_STAMP_WGS = 4096;   // [6..9] (ABL 256): K-loop cycles in vmcnt waits,
+                                                       // barriers, lgkmcnt waits, MFMA issue (wave 0)
 __device__ unsigned long long g_cv3_stamp[CV_STAMP_WGS * CV_STAMPS];
 template <typename K_, bool RELU, int BN, int EPI, int ABL = 0, int TH = 16>
 __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
@@ -151,9 +153,16 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
       for (int fn = 0; fn < QF; ++fn)
         bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((c0 & 127) + fn * 16 + frow, ks * 4 + fchunk));
   };
+  auto tick = [&]() -> unsigned long long {
+    if constexpr ((ABL & 256) != 0) return __builtin_amdgcn_s_memtime();
+    return 0ull;
+  };
   auto mma = [&](int qm, int qn) {
+    const unsigned long long m0_ = tick();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    const unsigned long long m1_ = tick();
+    if constexpr ((ABL & 256) != 0) st_[8] += m1_ - m0_;
     if constexpr (ABL & 4) return;
     __builtin_amdgcn_s_setprio(1);
     #pragma unroll
@@ -167,9 +176,12 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
           acc[qm * HQ + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * HQ + fm][qn * QF + fn]);
       }
     __builtin_amdgcn_s_setprio(0);
+    if constexpr ((ABL & 256) != 0) { __builtin_amdgcn_sched_barrier(0); st_[9] += tick() - m1_; }
   };
   auto bar = [&]() {
+    const unsigned long long b0_ = tick();
     if constexpr ((ABL & 16) == 0) asm volatile("s_barrier" ::: "memory");
+    if constexpr ((ABL & 256) != 0) st_[7] += tick() - b0_;
   };
 
   // K loop: per K step (channel block cb, tap) two half-step phases {fragment reads, LDS-DMA,
@@ -207,8 +219,10 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     bar(); mma(0, 0); mma(0, 1); bar();
     readA(1, pb, ky, kx);
     if (n2 && !(ABL & 2) && !(ABL & 64)) issue_b(0, t + 2);
+    const unsigned long long v0_ = tick();
     if (np) { if (n2) wait_vmcnt<PPW + 2>(); else wait_vmcnt<PPW>(); }
     else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
+    if constexpr ((ABL & 256) != 0) st_[6] += tick() - v0_;
     if (NBH == 2 && n2 && !(ABL & 2) && !(ABL & 64)) issue_b(1, t + 2);
     bar(); mma(1, 0); mma(1, 1); bar();
   }
@@ -388,9 +402,10 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
   p.tiles_n = p.N / bn;
   p.tiles_m = (p.M / (S * S)) * (S / th) * (S / CV_TW);
   dim3 grid(p.tiles_m * p.tiles_n);
-  const int abl = p.dbg & 255;
+  const int abl = p.dbg & 511;
   if (th == 12) {
     if (abl == 8 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 8, 12>), grid, dim3(512), 0, s, p);
+    else if (abl == 264 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 264, 12>), grid, dim3(512), 0, s, p);
     else if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 0, 12>), grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 256, CV_EPI_RES, 0, 12>), grid, dim3(512), 0, s, p);
     DP_CHECK_LAUNCH();
@@ -404,7 +419,7 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
 #define DP_CV3A(A_) case A_: hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, A_>), grid, dim3(512), 0, s, p); break;
       DP_CV3A(1) DP_CV3A(2) DP_CV3A(3) DP_CV3A(4) DP_CV3A(5) DP_CV3A(6) DP_CV3A(7) DP_CV3A(8)
       DP_CV3A(10) DP_CV3A(12) DP_CV3A(14) DP_CV3A(24) DP_CV3A(26) DP_CV3A(28) DP_CV3A(30) DP_CV3A(40) DP_CV3A(72)
-      DP_CV3A(136)
+      DP_CV3A(136) DP_CV3A(264)
 #undef DP_CV3A
     }
   } else if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);

@@ -61,10 +61,10 @@ def main():
         print(f"{lab}: {1000 * e0.elapsed_time(e1) / n:.1f} us per launch ({n} launches)")
     lib.dp_gemm_debug_flags(0)
     nwg = (S // 16) * (S // args.th)
-    buf = (ctypes.c_ulonglong * (nwg * 6))()
+    buf = (ctypes.c_ulonglong * (nwg * 10))()
     lib.dp_cv3_stamps.restype = ctypes.c_int
     assert lib.dp_cv3_stamps(buf, nwg) == 0
-    st = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 6).astype(np.float64)
+    st = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 10).astype(np.float64)
     clk = (st[:, 3] - st[:, 0]) / ((st[:, 5] - st[:, 4]) / 100e6)   # shader cycles / s
     mhz = np.median(clk) / 1e6
     pro, loop, epi = st[:, 1] - st[:, 0], st[:, 2] - st[:, 1], st[:, 3] - st[:, 2]
@@ -75,6 +75,9 @@ def main():
                    ("workgroup", tot)):
         print(f"  {lab:36s} median {np.median(v):9.0f} cyc = {np.median(v) / mhz:7.2f} us  "
               f"(p10 {np.percentile(v, 10) / mhz:6.2f}, p90 {np.percentile(v, 90) / mhz:6.2f})")
+    if args.abl & 256:
+        for j, lab in ((6, "vmcnt waits"), (7, "barriers"), (8, "lgkmcnt waits before MFMAs"), (9, "MFMA issue")):
+            print(f"  wave 0, K loop: {lab:28s} {np.median(st[:, j]) / kt:7.0f} cyc per step")
     print(f"  K loop per step: {np.median(loop) / kt:.0f} cyc (MFMA floor 2 waves x {8 * args.th // 2} MFMAs x 16 = {128 * args.th})")
     # workgroup rounds: start-time spread
     t0 = st[:, 0] - st[:, 0].min()
