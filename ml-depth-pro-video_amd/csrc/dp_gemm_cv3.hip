@@ -44,7 +44,8 @@ constexpr int CV_EPI_RES = 0, CV_EPI_BC = 1, CV_EPI_HPS = 2;
 // normal kernel plus per-workgroup clock stamps into g_cv3_stamp (tools/cv3_stamps.py); 16: no
 // barriers in the K loop; 32: the A fragments' ReLU applied by the reading wave; 64: no weight
 // LDS-DMA in the K loop; 128: no patch LDS-DMA in the K loop; 256 (with 8): wave 0's K-loop cycles by
-// kind into stamps 6..9
+// kind into stamps 6..9; 512: static priority (waves 4-7 at
+// priority 1 through the K loop) instead of a raise / drop around every MFMA run
 constexpr int CV_STAMPS = 10, CV_STAMP_WGS = 4096;   // [6..9] (ABL 256): K-loop cycles in vmcnt waits,
                                                        // barriers, lgkmcnt waits, MFMA issue (wave 0)
 __device__ unsigned long long g_cv3_stamp[CV_STAMP_WGS * CV_STAMPS];
@@ -164,7 +165,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     const unsigned long long m1_ = tick();
     if constexpr ((ABL & 256) != 0) st_[8] += m1_ - m0_;
     if constexpr (ABL & 4) return;
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr ((ABL & 512) == 0) __builtin_amdgcn_s_setprio(1);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
@@ -175,7 +176,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
         for (int fn = 0; fn < QF; ++fn)
           acc[qm * HQ + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * HQ + fm][qn * QF + fn]);
       }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr ((ABL & 512) == 0) __builtin_amdgcn_s_setprio(0);
     if constexpr ((ABL & 256) != 0) { __builtin_amdgcn_sched_barrier(0); st_[9] += tick() - m1_; }
   };
   auto bar = [&]() {
@@ -201,6 +202,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   }
   lds_barrier();
   if constexpr ((ABL & 8) != 0) st_[1] = __builtin_amdgcn_s_memtime();
+  if constexpr ((ABL & 512) != 0) { if (wave_u >= 4) __builtin_amdgcn_s_setprio(1); }
   if (wm == 1) bar();
   for (int t = 0; t < KT; ++t) {
     const int cb = t / 9, tap = t - cb * 9, ky = tap / 3, kx = tap - ky * 3;
@@ -227,6 +229,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     bar(); mma(1, 0); mma(1, 1); bar();
   }
   if (wm == 0) bar();
+  if constexpr ((ABL & 512) != 0) __builtin_amdgcn_s_setprio(0);
 
   // epilogues in the MFMA register layout: fragment row fm of the wave is output pixel row
   // wm * FM + fm of the tile (16 consecutive pixels, lane & 15), each lane 4 consecutive
@@ -402,9 +405,10 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
   p.tiles_n = p.N / bn;
   p.tiles_m = (p.M / (S * S)) * (S / th) * (S / CV_TW);
   dim3 grid(p.tiles_m * p.tiles_n);
-  const int abl = p.dbg & 511;
+  const int abl = p.dbg & 1023;
   if (th == 12) {
     if (abl == 8 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 8, 12>), grid, dim3(512), 0, s, p);
+    else if (abl == 520 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 520, 12>), grid, dim3(512), 0, s, p);
     else if (abl == 264 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 264, 12>), grid, dim3(512), 0, s, p);
     else if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 0, 12>), grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 256, CV_EPI_RES, 0, 12>), grid, dim3(512), 0, s, p);
@@ -419,7 +423,7 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
 #define DP_CV3A(A_) case A_: hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, A_>), grid, dim3(512), 0, s, p); break;
       DP_CV3A(1) DP_CV3A(2) DP_CV3A(3) DP_CV3A(4) DP_CV3A(5) DP_CV3A(6) DP_CV3A(7) DP_CV3A(8)
       DP_CV3A(10) DP_CV3A(12) DP_CV3A(14) DP_CV3A(24) DP_CV3A(26) DP_CV3A(28) DP_CV3A(30) DP_CV3A(40) DP_CV3A(72)
-      DP_CV3A(136) DP_CV3A(264)
+      DP_CV3A(136) DP_CV3A(264) DP_CV3A(520)
 #undef DP_CV3A
     }
   } else if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);
