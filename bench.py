@@ -255,7 +255,8 @@ def timed_steps(infer_one, steps: int, warmup: int, world: int, dev: torch.devic
 
 # environment switches and their product defaults: a bench line is only printed for the defaults
 AB_KNOBS = {"DP_ABLATE": "0", "DP_GEMM_DEBUG": "0", "DP_ATTN_DEBUG": "0", "DP_SIDE_GATE": "0", "DP_LN_FOLD": "1",
-            "DP_LN_SPLIT": "1", "DP_DEC_EARLY": "1", "DP_QKV_P8": "1", "DP_LN_RS": "1"}
+            "DP_LN_SPLIT": "1", "DP_DEC_EARLY": "1", "DP_QKV_P8": "1", "DP_LN_RS": "1",
+            "DP_SPLITK_DEC": "4"}
 
 
 def main():

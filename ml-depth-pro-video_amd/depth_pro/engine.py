@@ -23,7 +23,8 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from . import ops
-from ._lib import DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DP_TILE_P8PH_256x256, DPError, load
+from ._lib import (DP_ACT_GELU, DP_ACT_RELU, DP_BF16, DP_F16, DP_F32, DP_TILE_P8PH_256x256, DP_TILE_SPLITK_256x256,
+                   DPError, load)
 from .spec import DEPTH, EMBED_DIM, HEADS, IMG_SIZE, MLP_DIM, TOKENS
 
 # Timing ablations for tools/frame_ablation.py only (results are wrong when set):
@@ -475,6 +476,12 @@ class Engine:
         self.last_status: Optional[FrameStatus] = None
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
         self.dec_early = os.environ.get("DP_DEC_EARLY", "1") == "1"
+        # small-grid GEMMs of the main stream's post-encoder chain on the split-K engine: "4" the
+        # decoder's convs.4 (1024 -> 256 3x3 at 48^2: 9 tiles, 103 -> 41 us alone), "3" convs.3 (96^2,
+        # dec_c), "u" upsample2.0 (24^2 x 1024, 24 tiles), "f" fuse_lowres (48^2 x 1024, K 2048); "0"
+        # the planner's choice.  Default "4": +0.23 / +0.12 / +0.09 fps in three same-box A/Bs, "4uf"
+        # +0.1 / -0.05, "34uf" -0.07 (profiles/r05ah_splitk_dec/); depth rel-L1 8.741e-4 -> 8.769e-4
+        self.splitk_dec = os.environ.get("DP_SPLITK_DEC", "4")
         # the patch encoder's folded qkv on the persistent 8-phase engine (+ the LN merge pre-pass), as
         # fc1: 948 tiles of 256 x 256 over 256 workgroups instead of 3 rounds of 320 x 256 tiles, each
         # tile's epilogue under the next one's K loop: 48.41 / 48.27 -> 49.14 / 49.06 fps same box
@@ -614,12 +621,12 @@ class Engine:
 
     # -------------------------------------------------------- conv helpers
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
-               stride=1, border_corr=None):
+               stride=1, border_corr=None, tile=0):
         s_out = (s_in + 2 - 3) // stride + 1
         ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
                  conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
                  relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout, ldc=cout,
-                 border_corr=border_corr)
+                 border_corr=border_corr, tile=tile)
 
     def _deconv(self, x, s_in, cin, w, out, cout, bias=None, C_off=0, ldc=None):
         ops.gemm(x, w, out, M=s_in * s_in, N=4 * cout, K=cin, bias=bias, deconv=(s_in, s_in, cout),
@@ -801,13 +808,17 @@ class Engine:
             self._deconv(self.t96_512, 96, 512, P[e + "upsample0.1"], self.enc2, 512)
             ev["enc2"] = mark(self.dec_b)
         lat1_chain()
-        ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
+        sk = DP_TILE_SPLITK_256x256
+        ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D,
+                 tile=sk if "u" in self.splitk_dec else 0)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
         if not serial:
             main.wait_stream(self.side)  # join: the image-encoder half of `cat`
-        ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
+        ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"],
+                 tile=sk if "f" in self.splitk_dec else 0)
         # decoder (decoder.py:74-93)
-        self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256)
+        self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256,
+                    tile=sk if "4" in self.splitk_dec else 0)
         # dec_c (after convs.4, the main stream's last stream-K launch before fusion 1's deconv, which
         # waits for convs.1 -- so dec_c's stream-K launches never overlap the main stream's):
         # convs.3 / .2 / .1 in the order the fusions need them, the lat0 chain's 384^2 -> 768^2
@@ -817,7 +828,8 @@ class Engine:
                                       (1, (self.enc1, 384, 256))):
                 if not serial:
                     self.dec_c.wait_event(ev[f"enc{i}"])
-                self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256)
+                self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256,
+                            tile=DP_TILE_SPLITK_256x256 if str(i) in self.splitk_dec and i >= 3 else 0)
                 ev[f"c{i}"] = mark(self.dec_c)
             if not serial:
                 self.dec_c.wait_event(ev["lat0pre"])

@@ -109,7 +109,9 @@ def test_gemm_plan_tile_choice():
     wsk = dict(workspace=256, workspace_bytes=ws)
     assert conv(48, 1024, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 9 * 6)     # 9 tiles x split 6
     assert conv(96, 1024, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 36 * 6)    # 36 tiles x split 6
-    assert conv(192, 512, **wsk)[1:] == (_lib.DP_TILE_STREAMK_256x256, 256)       # 144 tiles over 256 CUs
+    # 192^2 x 512 channels: 144 tiles of 16 x 16 px would leave 112 CUs idle -- 12-row patch-conv tiles
+    # (192 workgroups, one round; the planner rule of DP_TILE_CV3_192x256)
+    assert conv(192, 512, **wsk)[1:] == (_lib.DP_TILE_CV3_192x256, 192)
     assert conv(48, 1024)[1] != _lib.DP_TILE_STREAMK_256x256                        # no workspace
     assert conv(48, 256, **wsk)[1] == _lib.DP_TILE_BIG_256x128                     # K = 2304
     # split-K + reduce: an explicit hint (needs a workspace); split = min(CUs / tiles, K steps / 2,
