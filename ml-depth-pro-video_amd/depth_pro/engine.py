@@ -478,7 +478,8 @@ class Engine:
         self.dec_early = os.environ.get("DP_DEC_EARLY", "1") == "1"
         # small-grid GEMMs of the main stream's post-encoder chain on the split-K engine: "4" the
         # decoder's convs.4 (1024 -> 256 3x3 at 48^2: 9 tiles, 103 -> 41 us alone), "3" convs.3 (96^2,
-        # dec_c), "u" upsample2.0 (24^2 x 1024, 24 tiles), "f" fuse_lowres (48^2 x 1024, K 2048); "0"
+        # dec_c), "u" upsample2.0 (24^2 x 1024, 24 tiles), "f" fuse_lowres (48^2 x 1024, K 2048), "r" the
+        # fusions' 48^2 / 96^2 ResidualBlock convs (50 -> 36, 52 -> 43 us alone, but -0.2 fps in-frame); "0"
         # the planner's choice.  Default "4": +0.23 / +0.12 / +0.09 fps in three same-box A/Bs, "4uf"
         # +0.1 / -0.05, "34uf" -0.07 (profiles/r05ah_splitk_dec/); depth rel-L1 8.741e-4 -> 8.769e-4
         self.splitk_dec = os.environ.get("DP_SPLITK_DEC", "4")
@@ -623,6 +624,8 @@ class Engine:
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
                stride=1, border_corr=None, tile=0):
         s_out = (s_in + 2 - 3) // stride + 1
+        if not tile and "r" in self.splitk_dec and s_in in (48, 96) and stride == 1 and cin == 256 and cout == 256:
+            tile = DP_TILE_SPLITK_256x256     # the fusions' 48^2 / 96^2 ResidualBlock convs (main stream)
         ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
                  conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
                  relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout, ldc=cout,
