@@ -41,7 +41,7 @@ enum { DP_A_DENSE = 0, DP_A_CONV = 1 };
 enum { DP_STORE_ROWS = 0, DP_STORE_DECONV2X2 = 1, DP_STORE_HEAD_PS = 2 };
 
 /* ABI version of this header; the Python loader refuses a mismatching .so. */
-#define DP_ABI_VERSION 13
+#define DP_ABI_VERSION 14
 int dp_abi_version(void);
 
 /*
@@ -166,7 +166,7 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
        DP_TILE_BIG_320x256 = 13, DP_TILE_BIG_512x128 = 14, DP_TILE_PBIG_320x256 = 15,
        DP_TILE_PBIG_256x256 = 16, DP_TILE_DUAL_256x128 = 17,
        DP_TILE_P8PH_256x256 = 18, DP_TILE_8PH_320x256 = 19, DP_TILE_CV3_256x256 = 20,
-       DP_TILE_SPLITK_256x256 = 21, DP_TILE_CV3_192x256 = 22 };
+       DP_TILE_SPLITK_256x256 = 21, DP_TILE_CV3_192x256 = 22, DP_TILE_CV3_384x128 = 23 };
 /* DP_TILE_P8PH_256x256: persistent 8-phase engine (min(tiles, CUs) workgroups, each a stream of
    K steps over its tiles; dense A, N % 256 == 0, K >= 128, 16-bit C without per-row operands);
    the auto choice for the ViT fc1.  DP_TILE_8PH_320x256: 8-phase 320 x 256 engine (dense A, no
@@ -179,6 +179,9 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
    DP_TILE_CV3_192x256: the same engine on 12 x 16-pixel tiles (side % 48 == 0, N % 256 == 0, the
    ReLU / residual epilogues): the auto choice where those tiles make whole rounds of workgroups and
    16 x 16 ones do not (the 384^2 ResidualBlock convs and projection: 768 tiles = 3 rounds).
+   DP_TILE_CV3_384x128 (ABI 14): the same engine on 24 x 16-pixel tiles of 128 output channels
+   (side % 48 == 0, N % 128 == 0, the border-corrected composed conv with head_corr only): the auto
+   choice for that conv (out_conv∘head.0 at 768^2: 1536 tiles = 6 rounds).
    DP_TILE_SPLITK_256x256 (ABI 11, a hint only, needs a workspace): split-K for small grids -- the
    256 x 256 tiles' K steps split over up to (CUs / tiles) workgroups that write fp32 partials into
    the workspace, then a reduce launch sums them in split order and runs the epilogue

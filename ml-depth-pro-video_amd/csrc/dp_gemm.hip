@@ -35,6 +35,7 @@ int launch_tile(const GemmP& p, int tile, bool conv, bool bf16, hipStream_t s) {
     case DP_TILE_8PH_320x256: return launch_part_8ph320(p, conv, bf16, s);
     case DP_TILE_CV3_256x256: return launch_part_cv3(p, conv, bf16, s);
     case DP_TILE_CV3_192x256: return launch_part_cv3(p, conv, bf16, s, 12);
+    case DP_TILE_CV3_384x128: return launch_part_cv3(p, conv, bf16, s, 24);
     case DP_TILE_BIG_320x256: case DP_TILE_BIG_512x128: return launch_part_big320(p, tile, conv, bf16, s);
     default: return launch_part_big(p, tile, conv, bf16, s);
   }
@@ -155,13 +156,15 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     else if (a->N <= 64) tile = DP_TILE_256x64;
     else if (a->N % 8 != 0) tile = DP_TILE_128x128;
     else if (a->N == 128 && a->M >= 512 * 256) {   // N = 128 convs at 768^2: the head.0 conv
-      // the patch-conv engine for the stride-1 square ones (the composed out_conv∘head.0); A/B:
-      // debug 4096 = the 512 x 128 engine
+      // the patch-conv engine for the stride-1 square ones (the composed out_conv∘head.0), on
+      // 24 x 16-pixel tiles where the side allows (48 MFMAs per wave and K step instead of 32); A/B:
+      // debug 4096 = the 512 x 128 engine, 1 << 29 = the 16 x 16-pixel tiles
       const bool cv3 = a->a_mode == DP_A_CONV && a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 &&
                        a->in_h == a->in_w && a->out_h == a->in_h && a->out_w == a->in_w && a->in_w % 16 == 0 &&
                        a->in_c % 64 == 0 && a->head_corr && a->store_mode == DP_STORE_ROWS && a->c_dtype != DP_F32 &&
                        !a->R1 && !a->R2 && !a->gamma && !a->pos && !a->accumulate && !a->row_group && !(dbg & 4096);
-      tile = cv3 ? DP_TILE_CV3_256x256 : DP_TILE_BIG_512x128;
+      tile = !cv3 ? DP_TILE_BIG_512x128
+             : (a->in_w % 48 == 0 && !(dbg & (1 << 29))) ? DP_TILE_CV3_384x128 : DP_TILE_CV3_256x256;
     }
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
     else if (ws_ok && a->a_mode == DP_A_CONV && !(dbg & 32) && tiles256 < num_cus() &&
@@ -335,8 +338,10 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   }
   if (tile >= DP_TILE_BIG_256x256 && a->N % 8 != 0) return DP_ERR_SHAPE;  // 8-column epilogue chunks
   // the border-corrected composed conv exists in the 512 x 128 conv engine only
-  if (a->store_mode == DP_STORE_ROWS && a->head_corr && tile != DP_TILE_BIG_512x128 && tile != DP_TILE_CV3_256x256)
+  if (a->store_mode == DP_STORE_ROWS && a->head_corr && tile != DP_TILE_BIG_512x128 && tile != DP_TILE_CV3_256x256 &&
+      tile != DP_TILE_CV3_384x128)
     return DP_ERR_ARG;
+  if (tile == DP_TILE_CV3_384x128 && (!a->head_corr || a->store_mode != DP_STORE_ROWS || a->N != 128)) return DP_ERR_ARG;
 
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
@@ -390,6 +395,7 @@ extern "C" int dp_gemm_plan(const dp_gemm_args* a, int32_t* tile_out, int32_t* g
     case DP_TILE_DUAL_256x128: bn = 128; break;
     case DP_TILE_PBIG_320x256: case DP_TILE_8PH_320x256: bm = 320; bn = 256; break;
     case DP_TILE_CV3_192x256: bm = 192; bn = 256; break;
+    case DP_TILE_CV3_384x128: bm = 384; bn = 128; break;
     default: bn = 256;
   }
   if (tile_out) *tile_out = tile;

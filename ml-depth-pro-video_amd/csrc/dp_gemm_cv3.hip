@@ -24,12 +24,13 @@ namespace {
 
 // Output tiles of TH x 16 pixels: TH = 16 (the 768^2 maps: 2304 tiles = 9 rounds of 256 CUs) or
 // TH = 12 (DP_TILE_CV3_192x256, the 384^2 maps: 768 tiles = 3 rounds exactly, where 16 x 16 tiles
-// make 2.25 rounds); the patch is (TH + 2) x 18 pixels.
+// make 2.25 rounds), or TH = 24 (DP_TILE_CV3_384x128, the 128-channel head conv at 768^2: 1536 tiles =
+// 6 rounds; 48 MFMAs per wave and K step instead of 32); the patch is (TH + 2) x 18 pixels.
 constexpr int CV_TW = 16;                     // output tile width (pixels)
 constexpr int CV_PW = CV_TW + 2;              // patch width
 template <int TH> struct CvGeo {
-  static constexpr int PIX = (TH + 2) * CV_PW;              // patch pixels (324 / 252)
-  static constexpr int PPW = (PIX * 8 + 511) / 512;          // LDS-DMA pieces per wave (6 / 4)
+  static constexpr int PIX = (TH + 2) * CV_PW;              // patch pixels (324 / 252 / 468)
+  static constexpr int PPW = (PIX * 8 + 511) / 512;          // LDS-DMA pieces per wave (6 / 4 / 8)
   static constexpr int PATCH_B = 8 * PPW * 1024;             // bytes per patch buffer
   static constexpr int FM = TH / 2, HQ = FM / 2;             // fragment rows per wave / per phase
 };
@@ -54,7 +55,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   using G = CvGeo<TH>;
   constexpr int FM = G::FM, HQ = G::HQ, PPW = G::PPW, CV_PATCH_B = G::PATCH_B, CV_PIX = G::PIX;
   constexpr int TN = BN / 4, FN = TN / 16, QF = FN / 2;          // wave tile 16 FM x TN
-  static_assert(TH == 16 || TH == 12, "tile rows");
+  static_assert(TH == 16 || TH == 12 || (TH == 24 && BN == 128), "tile rows");
   constexpr int NBH = BN / 128;                                  // weight halves per K step
   constexpr int B_B = BN * 128;                                  // bytes per weight K step
   static_assert(EPI != CV_EPI_RES || BN == 256, "residual epilogue: BN 256");
@@ -402,10 +403,17 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
     return DP_ERR_ARG;
   }
   if (th == 12 && epi != CV_EPI_RES) return DP_ERR_ARG;   // (12-row tiles: the ResidualBlock-type convs only)
+  if (th == 24 && (epi != CV_EPI_BC || bn != 128)) return DP_ERR_ARG;   // (24-row tiles: the 128-channel head conv)
   p.tiles_n = p.N / bn;
   p.tiles_m = (p.M / (S * S)) * (S / th) * (S / CV_TW);
   dim3 grid(p.tiles_m * p.tiles_n);
   const int abl = p.dbg & 1023;
+  if (th == 24) {   // 24 x 16-pixel tiles, 128 channels: 2 x 64 KiB patches + 2 x 16 KiB weight steps
+    if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 128, CV_EPI_BC, 0, 24>), grid, dim3(512), 0, s, p);
+    else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 128, CV_EPI_BC, 0, 24>), grid, dim3(512), 0, s, p);
+    DP_CHECK_LAUNCH();
+    return 0;
+  }
   if (th == 12) {
     if (abl == 8 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 8, 12>), grid, dim3(512), 0, s, p);
     else if (abl == 520 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 520, 12>), grid, dim3(512), 0, s, p);

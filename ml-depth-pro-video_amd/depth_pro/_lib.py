@@ -26,8 +26,8 @@ INTERP_MODES = {"bilinear": DP_INTERP_BILINEAR, "bicubic": DP_INTERP_BICUBIC}
  DP_TILE_DEEP5_256x256, DP_TILE_DEEP_256x128, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256,
  DP_TILE_BIG_512x128, DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128,
  DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256, DP_TILE_SPLITK_256x256,
- DP_TILE_CV3_192x256) = range(23)
-DP_ABI_VERSION = 13
+ DP_TILE_CV3_192x256, DP_TILE_CV3_384x128) = range(24)
+DP_ABI_VERSION = 14
 
 _ERRORS = {1000: "DP_ERR_ARG", 1001: "DP_ERR_SHAPE", 1002: "DP_ERR_ALIGN", 1003: "DP_ERR_DTYPE"}
 

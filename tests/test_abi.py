@@ -133,7 +133,8 @@ def test_gemm_plan_tile_choice():
                     stride=1, pad=1, out_h=768, out_w=768, head_corr=256, **kw)
     h0c = dict(cin=256, in_c=256)
     hps = dict(cin=128, in_c=128, store_mode=_lib.DP_STORE_HEAD_PS, head_w=256, c_dtype=_lib.DP_F32)
-    assert head(**h0c)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
+    assert head(**h0c)[1:] == (_lib.DP_TILE_CV3_384x128, 1536)                       # 24 x 16-pixel tiles
+    assert head(**h0c, tile=_lib.DP_TILE_CV3_256x256)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
     assert head(**hps)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)
     assert head(**hps, tile=_lib.DP_TILE_CV3_256x256)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
     # the decoder's 2x2 deconvs with >= 128 tiles of 256 x 256: the persistent 8-phase engine with

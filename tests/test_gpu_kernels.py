@@ -946,10 +946,11 @@ def test_patch_conv3x3_planner_tiles(cuda):
 @pytest.mark.parametrize("dt", DTYPES)
 def test_patch_conv3x3_head_epilogues(cuda, dt):
     """The patch-conv engine's head convs (128 output channels per tile): the border-corrected
-    composed conv (out_conv∘head.0) bit-identical to the 512 x 128 engine, and the composed depth
+    composed conv (out_conv∘head.0) bit-identical to the 512 x 128 engine on 16 x 16- and 24 x 16-pixel
+    tiles (DP_TILE_CV3_384x128, 4 x 6 tiles of a 96^2 map), and the composed depth
     head (HEAD_PS: deconv∘3x3∘ReLU∘1x1∘ReLU, one parity per wave) equal to it up to the order of
     the 32-channel dot product; both against the reference layer order in fp32."""
-    from depth_pro._lib import DP_TILE_CV3_256x256
+    from depth_pro._lib import DP_TILE_CV3_256x256, DP_TILE_CV3_384x128
     from depth_pro.engine import compose_head, compose_head0
 
     g = torch.Generator().manual_seed(43)
@@ -969,8 +970,11 @@ def test_patch_conv3x3_head_epilogues(cuda, dt):
     out2 = out1.clone()
     ops.gemm(x, P["head.0c.w"], out1, tile=DP_TILE_CV3_256x256, **kw)
     ops.gemm(x, P["head.0c.w"], out2, tile=DP_TILE_BIG_512x128, **kw)
+    out3 = torch.full_like(out1, float("nan"))
+    ops.gemm(x, P["head.0c.w"], out3, tile=DP_TILE_CV3_384x128, **kw)
     torch.cuda.synchronize()
     assert torch.equal(out1, out2), (out1.float() - out2.float()).abs().max().item()
+    assert torch.equal(out3, out2), (out3.float() - out2.float()).abs().max().item()
     close(out1, ref, dt, "cv3 border-corrected composed conv")
 
     ci, H = 128, 48

@@ -13,7 +13,7 @@ from depth_pro._lib import (DP_TILE_128x128, DP_TILE_256x64, DP_TILE_8PH_256x256
                             DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256, DP_TILE_BIG_512x128,
                             DP_TILE_PBIG_320x256, DP_TILE_PBIG_256x256, DP_TILE_DUAL_256x128,
                             DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256,
-                            DP_TILE_SPLITK_256x256, DP_TILE_CV3_192x256)
+                            DP_TILE_SPLITK_256x256, DP_TILE_CV3_192x256, DP_TILE_CV3_384x128)
 
 TILES = (("auto", 0), ("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TILE_BIG_256x128),
          ("8ph256x256", DP_TILE_8PH_256x256), ("deep4_256x256", DP_TILE_DEEP4_256x256),
@@ -23,7 +23,8 @@ TILES = (("auto", 0), ("big256x256", DP_TILE_BIG_256x256), ("big256x128", DP_TIL
          ("pbig320x256", DP_TILE_PBIG_320x256), ("pbig256x256", DP_TILE_PBIG_256x256),
          ("dual256x128", DP_TILE_DUAL_256x128), ("p8ph256x256", DP_TILE_P8PH_256x256),
          ("8ph320x256", DP_TILE_8PH_320x256), ("cv3_256x256", DP_TILE_CV3_256x256),
-         ("splitk256x256", DP_TILE_SPLITK_256x256), ("cv3_192x256", DP_TILE_CV3_192x256))
+         ("splitk256x256", DP_TILE_SPLITK_256x256), ("cv3_192x256", DP_TILE_CV3_192x256),
+         ("cv3_384x128", DP_TILE_CV3_384x128))
 N256 = (DP_TILE_BIG_256x256, DP_TILE_BIG_256x256_K32, DP_TILE_8PH_256x256, DP_TILE_DEEP4_256x256,
         DP_TILE_DEEP5_256x256, DP_TILE_STREAMK_256x256, DP_TILE_BIG_320x256, DP_TILE_PBIG_320x256,
         DP_TILE_PBIG_256x256, DP_TILE_P8PH_256x256, DP_TILE_8PH_320x256, DP_TILE_CV3_256x256,
