@@ -403,13 +403,14 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
     return DP_ERR_ARG;
   }
   if (th == 12 && epi != CV_EPI_RES) return DP_ERR_ARG;   // (12-row tiles: the ResidualBlock-type convs only)
-  if (th == 24 && (epi != CV_EPI_BC || bn != 128)) return DP_ERR_ARG;   // (24-row tiles: the 128-channel head conv)
+  if (th == 24 && ((epi != CV_EPI_BC && epi != CV_EPI_HPS) || bn != 128)) return DP_ERR_ARG;   // (the 128-channel head convs)
   p.tiles_n = p.N / bn;
   p.tiles_m = (p.M / (S * S)) * (S / th) * (S / CV_TW);
   dim3 grid(p.tiles_m * p.tiles_n);
   const int abl = p.dbg & 1023;
   if (th == 24) {   // 24 x 16-pixel tiles, 128 channels: 2 x 64 KiB patches + 2 x 16 KiB weight steps
-    if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 128, CV_EPI_BC, 0, 24>), grid, dim3(512), 0, s, p);
+    if (epi == CV_EPI_HPS) hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 128, CV_EPI_HPS, 0, 24>), grid, dim3(512), 0, s, p);
+    else if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 128, CV_EPI_BC, 0, 24>), grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 128, CV_EPI_BC, 0, 24>), grid, dim3(512), 0, s, p);
     DP_CHECK_LAUNCH();
     return 0;

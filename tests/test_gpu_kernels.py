@@ -992,9 +992,12 @@ def test_patch_conv3x3_head_epilogues(cuda, dt):
     d2 = d1.clone()
     ops.gemm(xh, Q["head.ps.w"], d1, tile=DP_TILE_CV3_256x256, **kh)
     ops.gemm(xh, Q["head.ps.w"], d2, tile=DP_TILE_BIG_512x128, **kh)
+    d3 = torch.full_like(d1, float("nan"))
+    ops.gemm(xh, Q["head.ps.w"], d3, tile=DP_TILE_CV3_384x128, **kh)
     torch.cuda.synchronize()
     assert not torch.isnan(d1).any()
     assert (d1 - d2).abs().max().item() <= 1e-5 * (d2.abs().max().item() + 1e-6)
+    assert torch.equal(d3, d1)      # 24- and 16-row tiles: the same lanes sum the same products
     r = F.conv_transpose2d(h0, wd, bd, stride=2)
     r = F.relu(F.conv2d(F.relu(F.conv2d(r, w2, b2, padding=1)), w4.reshape(1, 32, 1, 1), torch.tensor([0.25])))
     close(d1, r[0, 0], dt, "cv3 head HEAD_PS")

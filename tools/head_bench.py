@@ -45,8 +45,9 @@ def main():
     conv = lambda cin: dict(in_h=S, in_w=S, in_c=cin, k=3, stride=1, pad=1, out_h=S, out_w=S)  # noqa: E731
     f0 = lambda: ops.gemm(feats, w0, h0, M=S * S, N=128, K=9 * 256, conv=conv(256), bias=b0,  # noqa: E731
                           border_corr=corr0)
+    ps_tile = int(os.environ.get("HEAD_PS_TILE", "0"))   # an explicit tile for head.ps (A/B)
     f1 = lambda: ops.gemm(h0, wps, out, M=S * S, N=128, K=9 * 128, conv=conv(128), bias=bps,  # noqa: E731
-                          head_w=hw, head_b=0.1, head_corr=corr)
+                          head_w=hw, head_b=0.1, head_corr=corr, tile=ps_tile)
     for lab, f, fl in (("head.0c (composed out_conv∘head.0)", f0, 2.0 * S * S * 128 * 2304),
                        ("head.ps (composed deconv + conv + 1x1)", f1, 2.0 * S * S * 128 * 1152)):
         us = timeit(f)
