@@ -144,7 +144,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     // 32-column parity groups must not straddle a wave's columns (TN = 32 or 64); the patch-conv
     // engine (one parity per wave) only when asked for: at 768^2 it runs 347 - 355 us in-frame vs
     // 249 - 255 on the 512 x 128 engine (profiles/r03w/)
-    if (tile != DP_TILE_CV3_256x256 && tile != DP_TILE_CV3_384x128)
+    if (tile != DP_TILE_CV3_256x256 && tile != DP_TILE_CV3_384x128 && tile != DP_TILE_BIG_256x128)
       tile = a->M >= 512 * 256 ? DP_TILE_BIG_512x128 : DP_TILE_BIG_256x128;
   } else if (a->head_w) {
     if (a->N > 32 || a->store_mode != DP_STORE_ROWS) return DP_ERR_SHAPE;

@@ -137,6 +137,9 @@ def test_gemm_plan_tile_choice():
     assert head(**h0c, tile=_lib.DP_TILE_CV3_256x256)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
     assert head(**hps)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)
     assert head(**hps, tile=_lib.DP_TILE_CV3_256x256)[1:] == (_lib.DP_TILE_CV3_256x256, 2304)
+    assert head(**hps, tile=_lib.DP_TILE_CV3_384x128)[1:] == (_lib.DP_TILE_CV3_384x128, 1536)
+    assert head(**hps, tile=_lib.DP_TILE_BIG_256x128)[1:] == (_lib.DP_TILE_BIG_256x128, 2304)
+    assert head(**hps, tile=_lib.DP_TILE_BIG_256x256)[1:] == (_lib.DP_TILE_BIG_512x128, 1152)    # not a HEAD_PS engine
     # the decoder's 2x2 deconvs with >= 128 tiles of 256 x 256: the persistent 8-phase engine with
     # the pixel-shuffle store; fewer tiles stay where they were
     def deconv(S, cin, cout, **kw):
