@@ -46,7 +46,8 @@ constexpr int CV_EPI_RES = 0, CV_EPI_BC = 1, CV_EPI_HPS = 2;
 // barriers in the K loop; 32: the A fragments' ReLU applied by the reading wave; 64: no weight
 // LDS-DMA in the K loop; 128: no patch LDS-DMA in the K loop; 256 (with 8): wave 0's K-loop cycles by
 // kind into stamps 6..9; 512: static priority (waves 4-7 at
-// priority 1 through the K loop) instead of a raise / drop around every MFMA run
+// priority 1 through the K loop) instead of a raise / drop around every MFMA run; 1024: no priority
+// changes at all
 constexpr int CV_STAMPS = 10, CV_STAMP_WGS = 4096;   // [6..9] (ABL 256): K-loop cycles in vmcnt waits,
                                                        // barriers, lgkmcnt waits, MFMA issue (wave 0)
 __device__ unsigned long long g_cv3_stamp[CV_STAMP_WGS * CV_STAMPS];
@@ -166,7 +167,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     const unsigned long long m1_ = tick();
     if constexpr ((ABL & 256) != 0) st_[8] += m1_ - m0_;
     if constexpr (ABL & 4) return;
-    if constexpr ((ABL & 512) == 0) __builtin_amdgcn_s_setprio(1);
+    if constexpr ((ABL & 1536) == 0) __builtin_amdgcn_s_setprio(1);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
@@ -177,7 +178,7 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
         for (int fn = 0; fn < QF; ++fn)
           acc[qm * HQ + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * HQ + fm][qn * QF + fn]);
       }
-    if constexpr ((ABL & 512) == 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr ((ABL & 1536) == 0) __builtin_amdgcn_s_setprio(0);
     if constexpr ((ABL & 256) != 0) { __builtin_amdgcn_sched_barrier(0); st_[9] += tick() - m1_; }
   };
   auto bar = [&]() {
@@ -407,7 +408,7 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
   p.tiles_n = p.N / bn;
   p.tiles_m = (p.M / (S * S)) * (S / th) * (S / CV_TW);
   dim3 grid(p.tiles_m * p.tiles_n);
-  const int abl = p.dbg & 1023;
+  const int abl = p.dbg & 2047;
   if (th == 24) {   // 24 x 16-pixel tiles, 128 channels: 2 x 64 KiB patches + 2 x 16 KiB weight steps
     if (epi == CV_EPI_HPS) hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 128, CV_EPI_HPS, 0, 24>), grid, dim3(512), 0, s, p);
     else if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 128, CV_EPI_BC, 0, 24>), grid, dim3(512), 0, s, p);
@@ -417,6 +418,7 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
   }
   if (th == 12) {
     if (abl == 8 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 8, 12>), grid, dim3(512), 0, s, p);
+    else if (abl == 1032 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 1032, 12>), grid, dim3(512), 0, s, p);
     else if (abl == 520 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 520, 12>), grid, dim3(512), 0, s, p);
     else if (abl == 264 && p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 264, 12>), grid, dim3(512), 0, s, p);
     else if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, 0, 12>), grid, dim3(512), 0, s, p);
@@ -432,7 +434,7 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
 #define DP_CV3A(A_) case A_: hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 256, CV_EPI_RES, A_>), grid, dim3(512), 0, s, p); break;
       DP_CV3A(1) DP_CV3A(2) DP_CV3A(3) DP_CV3A(4) DP_CV3A(5) DP_CV3A(6) DP_CV3A(7) DP_CV3A(8)
       DP_CV3A(10) DP_CV3A(12) DP_CV3A(14) DP_CV3A(24) DP_CV3A(26) DP_CV3A(28) DP_CV3A(30) DP_CV3A(40) DP_CV3A(72)
-      DP_CV3A(136) DP_CV3A(264) DP_CV3A(520)
+      DP_CV3A(136) DP_CV3A(264) DP_CV3A(520) DP_CV3A(1032)
 #undef DP_CV3A
     }
   } else if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);
