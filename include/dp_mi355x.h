@@ -180,8 +180,9 @@ enum { DP_TILE_AUTO = 0, DP_TILE_128x128 = 1, DP_TILE_256x64 = 2, DP_TILE_256x32
    ReLU / residual epilogues): the auto choice where those tiles make whole rounds of workgroups and
    16 x 16 ones do not (the 384^2 ResidualBlock convs and projection: 768 tiles = 3 rounds).
    DP_TILE_CV3_384x128 (ABI 14): the same engine on 24 x 16-pixel tiles of 128 output channels
-   (side % 48 == 0, N % 128 == 0, the border-corrected composed conv with head_corr only): the auto
-   choice for that conv (out_conv∘head.0 at 768^2: 1536 tiles = 6 rounds).
+   (side % 48 == 0, N == 128, with head_corr: the border-corrected composed conv, or
+   DP_STORE_HEAD_PS): the auto choice for the former (out_conv∘head.0 at 768^2: 1536 tiles =
+   6 rounds); a hint for the composed depth head, whose auto choice stays the 512 x 128 engine.
    DP_TILE_SPLITK_256x256 (ABI 11, a hint only, needs a workspace): split-K for small grids -- the
    256 x 256 tiles' K steps split over up to (CUs / tiles) workgroups that write fp32 partials into
    the workspace, then a reduce launch sums them in split order and runs the epilogue
