@@ -2418,14 +2418,22 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
 // s+1 in phase 3 -- so each piece has 4+ phases to land and the count is 8 in steady state.
 // Dense A only; epilogues: the load-free MFMA-layout one (EACT = DP_ACT_*; 16-bit C) or the
 // fp32 residual-accumulate one (EACT = EPI_ACC + act).
-template <typename K_, int EACT, int LNM = 0>   // LNM: 1 folded-LN producer, 2 consumer, 3 (4) producer on hi + lo
+// TCH (split producer only; debug 1 << 28, measured and rejected): the K loop's first steps also
+// stream the wave's epilogue rows of the residual (hi 20 KiB + lo 10 KiB, 30 LDS-DMA pieces into a
+// dummy 1 KiB LDS slot, TT per step), so the epilogue's own reads of them would hit the caches
+// instead of HBM: proj 71.1 -> 76.9 us cold, fc2 155.9 -> 162.5, in-frame -0.8 fps
+// (profiles/r05av_residual_touch/) -- the extra DMA issue in the K loop costs more than it saves
+template <typename K_, int EACT, int LNM = 0, bool TCH = false>   // LNM: 1 folded-LN producer, 2 consumer, 3 (4) producer on hi + lo
 __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   constexpr int BM = 320;
   constexpr int A_BYTES = BM * 128, B_BYTES = 256 * 128, BUF = A_BYTES + B_BYTES;
   constexpr int FM = 5, FN = 8, TM = 80, TN = 128;
   constexpr int RING = 2 * BUF;                                   // 144 KiB
   constexpr int PF = 1, SLAB = PF * 16 * TN * 2;                  // epilogue_mfma slab per wave
-  constexpr int SMEM = RING > 8 * SLAB ? RING : 8 * SLAB;
+  constexpr int SMEM0 = RING > 8 * SLAB ? RING : 8 * SLAB;
+  constexpr int SMEM = TCH ? SMEM0 + 8 * 1024 : SMEM0;            // + the touch slots
+  static_assert(!TCH || LNM == 3, "touch: the split producer");
+  constexpr int TT = TCH ? 3 : 0, TSTEPS = 10;                    // touch pieces per step, steps
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2456,6 +2464,22 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   };
   auto issueB = [&](int q, int t) {
     glds16(p.B + (boff + q * 32 * (int)p.ldb + t * 64), lds0 + (t & 1) * BUF + A_BYTES + (brow0 + q * 32) * 128);
+  };
+
+  // touch piece k of the wave's epilogue region (rows m0 + wm * 80 .., columns n0 + wn * 128 ..):
+  // k < 20: hi rows (k >> 2) * 16 + (k & 1) * 8 + lane / 8, column half (k >> 1) & 1; k >= 20: lo
+  // rows ((k - 20) >> 1) * 16 + lane / 4, column half (k - 20) & 1
+  auto touch = [&](int k) __attribute__((always_inline)) {
+    const uint32_t dst = lds0 + SMEM0 + wave_u * 1024;
+    const int mb = m0 + wm * TM, nb = n0 + wn * TN;
+    if (k < 20) {
+      const int m = min(mb + (k >> 2) * 16 + (k & 1) * 8 + (lane >> 3), p.M - 1);
+      glds16(p.ln_xb_out + (long long)m * p.ldc + nb + ((k >> 1) & 1) * 64 + (lane & 7) * 8, dst);
+    } else {
+      const int i = k - 20;
+      const int m = min(mb + (i >> 1) * 16 + (lane >> 2), p.M - 1);
+      glds16((const unsigned char*)p.ln_xl + (long long)m * p.ldc + nb + (i & 1) * 64 + (lane & 3) * 16, dst);
+    }
   };
 
   f32x4_t acc[FM][FN];
@@ -2512,27 +2536,39 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   for (int s = 0; s < KT; ++s) {
     const int buf = s & 1;
     const bool a1 = s + 1 < KT, a2 = s + 2 < KT;
+    // touch pieces of this step, issued after phase 0's wait: younger than everything phases 1-3
+    // retire (their counts + TT), older than what the next step's phase 0 retires
+    const bool tc = TCH && s < TSTEPS && s + 2 < KT;
     // phase 0: A fragments + B quarter 0; retire Bq1(s) (younger: 2 + 6 a1)
     readA(buf); readB(0, buf);
     if (a1) issueB(0, s + 1);
     if (a1) wait_vmcnt<8>(); else wait_vmcnt<2>();
+    if constexpr (TCH) {
+      if (tc) {
+        #pragma unroll
+        for (int k = 0; k < TT; ++k) touch(s * TT + k);
+      }
+    }
     bar(); mma(0); bar();
     // phase 1: retire Bq2(s) (younger: 1 + 7 a1)
     readB(1, buf);
     if (a1) issueB(1, s + 1);
-    if (a1) wait_vmcnt<8>(); else wait_vmcnt<1>();
+    if (tc) wait_vmcnt<8 + TT>();
+    else if (a1) wait_vmcnt<8>(); else wait_vmcnt<1>();
     bar(); mma(1); bar();
     // phase 2: A(s+2) pieces 0-2 into this step's buffer; retire Bq3(s) (younger: 5 a1 + 3 a2)
     readB(2, buf);
     if (a1) issueB(2, s + 1);
     if (a2) { issueA(0, s + 2); issueA(1, s + 2); issueA(2, s + 2); }
-    if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<5>(); else wait_vmcnt<0>();
+    if (tc) wait_vmcnt<8 + TT>();
+    else if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<5>(); else wait_vmcnt<0>();
     bar(); mma(2); bar();
     // phase 3: retire A(s+1) and Bq0(s+1) (younger: 3 + 5 a2)
     readB(3, buf);
     if (a1) issueB(3, s + 1);
     if (a2) { issueA(3, s + 2); issueA(4, s + 2); }
-    if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<3>();
+    if (tc) wait_vmcnt<8 + TT>();
+    else if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<3>();
     bar(); mma(3); bar();
   }
   if (wave < 4) bar();
@@ -2570,6 +2606,7 @@ int launch_8ph320(const GemmP& p0, hipStream_t s) {
     if (!p.ln_xb_out || p.act != DP_ACT_NONE) return DP_ERR_ARG;
     static_assert(8 * 13312 <= 2 * (320 * 128 + 256 * 128), "hi/lo staging fits the ring");
     if (p.dbg & (1 << 27)) hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 4>), grid, dim3(512), 0, s, p);
+    else if (p.dbg & (1 << 28)) hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3, true>), grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3>), grid, dim3(512), 0, s, p);
     DP_CHECK_LAUNCH();
     return 0;

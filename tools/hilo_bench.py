@@ -59,8 +59,8 @@ def main():
         res = []
         from depth_pro import _lib
         lib = _lib.load()
-        for lab, fn, dbg in (("fp32", f32, 0), ("split", spl, 0), ("split-ahead1", spl, 1 << 27),
-                             ("no-epilogue", spl, 1)):
+        for lab, fn, dbg in (("fp32", f32, 0), ("split", spl, 0), ("split-touch", spl, 1 << 28),
+                             ("split-ahead1", spl, 1 << 27), ("no-epilogue", spl, 1)):
             lib.dp_gemm_debug_flags(dbg)
             for cl, fl in (("warm", None), ("cold", flush)):
                 us = timeit(fn, 20, fl)
