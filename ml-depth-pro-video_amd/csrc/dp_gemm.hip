@@ -463,7 +463,9 @@ extern "C" int dp_gemm_grouped(const dp_gemm_args* a, int32_t groups, dp_stream_
   // 128 x 128 tiles: 2 x 577 rows in 10 row tiles, each workgroup a quarter of a 256 x 256 tile's
   // work, so the side workgroups that hold CUs when a one-round patch-encoder launch starts free
   // them sooner (in-frame: 48.39 -> 48.91 fps, fc1 172 -> 165 us, profiles/r04h_side_tiles/; 64 x
-  // 128: 48.47, profiles/r04i_side_tiles/).  Debug 1 << 26 (A/B): the 256 x 128 engine.
+  // 128: 48.47, profiles/r04i_side_tiles/; final round-5 tree: 49.81 / 50.38 / 50.23 / 49.98 vs
+  // 48.83 / 48.84 / 48.85 / 48.74 fps on 256 x 128, profiles/r05ay_side_tiles/).  Debug 1 << 26 (A/B):
+  // the 256 x 128 engine.
   const int gt = (p.dbg & (1 << 26)) ? DP_TILE_BIG_256x128 : TILE_GRP_128x128;
   return launch_part_big(p, gt, false, a->dtype == DP_BF16, s);
 }
