@@ -254,9 +254,7 @@ def timed_steps(infer_one, steps: int, warmup: int, world: int, dev: torch.devic
 
 
 # environment switches and their product defaults: a bench line is only printed for the defaults
-AB_KNOBS = {"DP_ABLATE": "0", "DP_GEMM_DEBUG": "0", "DP_ATTN_DEBUG": "0", "DP_SIDE_GATE": "0", "DP_LN_FOLD": "1",
-            "DP_LN_SPLIT": "1", "DP_DEC_EARLY": "1", "DP_QKV_P8": "1", "DP_LN_RS": "1",
-            "DP_SPLITK_DEC": "4"}
+AB_KNOBS = {"DP_ABLATE": "0", "DP_GEMM_DEBUG": "0"}
 
 
 def main():
@@ -296,7 +294,7 @@ def main():
 
     import depth_pro
     from depth_pro import distributed as D
-    from depth_pro import ops
+    from depth_pro import _lib, ops
     from depth_pro.depth_pro import DepthPro, DepthProConfig, Transform, _compute_dtype
     from depth_pro.engine import pack_weights
     from depth_pro.weights import synthetic_state_dict
@@ -419,10 +417,12 @@ def main():
             A = torch.empty(8, dtype=kdt, device=dev)
             tile, wgs = ops.gemm(A, A, A, M=M, N=N, K=K, plan_only=True, workspace=eng.ws_main)
             kname = tile_kernel(tile, kdt)
-            if tile == 18:
-                # the persistent engine runs both the folded-LN qkv and the GELU fc1 (round 5): the
-                # activation template argument tells them apart (the MLP up-projection, N = 4 K: GELU)
-                kname += ", false, 2," if N == 4 * K else ", false, 0,"
+            meta = ops.PROF_GEMM_META.get(dom_key)
+            if tile == _lib.DP_TILE_P8PH_256x256 and meta is not None:
+                # the persistent engine runs the folded-LN qkv and fc1 and the decoder's deconvs: its
+                # instantiation is <K_, RELU, ACT, HG, DCV, LNC> (dp_gemm_impl.h, launch_part_8ph)
+                b = lambda v: "true" if v else "false"  # noqa: E731
+                kname += f", false, {meta['act']}, false, {b(meta['deconv'])}, {b(meta['ln_consumer'])}>"
             dom_info["engine"] = {"tile": TILE_NAMES.get(tile, tile), "workgroups": wgs, "kernel": kname}
             traffic = pmc_traffic(kname, wgs) if kname else None
             if traffic is not None:
@@ -452,8 +452,10 @@ def main():
                        "graph": not args.no_graph,
                        "precision": {"bf16": "bf16 everywhere", "fp16": "f16 everywhere",
                                      "mixed": "bf16 MFMA operands in the three ViT-L encoders, f16 in the "
-                                              "encoder maps / decoder / heads (fp32 accumulate, fp32 ViT "
-                                              "residual stream): the default, chosen to meet depth L1 < 1e-3"
+                                              "encoder maps / decoder / heads (fp32 accumulate; the patch "
+                                              "encoder's residual stream held split as a 16-bit hi part + an "
+                                              "int8 lo part, ~16 significant bits, the side encoders' in "
+                                              "fp32): the default, chosen to meet depth L1 < 1e-3"
                                      }[args.dtype]},
             # dominant kernel: algorithmic FLOP per launch / its average HIP-event duration
             "roofline": {"bound": "mfma", "achieved": round(dom_tf, 1), "peak": PEAK_BF16_TFLOPS,

@@ -133,7 +133,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
                        !(a->workspace && a->workspace_bytes >= dp_gemm_workspace_size()) ||
                        (a->M + 319) / 320 > 1023 - LN_CNT_WORD))
     return DP_ERR_ARG;
-  if (a->ln_rs_in && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_P8PH_256x256) return DP_ERR_ARG;
+  if (a->ln_rs_in && ((a->tile != DP_TILE_AUTO && a->tile != DP_TILE_P8PH_256x256) || a->M < 2)) return DP_ERR_ARG;
   if ((lnp || lnc) && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_8PH_320x256 &&
       !(lnc && a->tile == DP_TILE_P8PH_256x256))   // (a consumer may ask for the persistent engine)
     return DP_ERR_ARG;
@@ -158,14 +158,14 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     else if (a->N % 8 != 0) tile = DP_TILE_128x128;
     else if (a->N == 128 && a->M >= 512 * 256) {   // N = 128 convs at 768^2: the head.0 conv
       // the patch-conv engine for the stride-1 square ones (the composed out_conv∘head.0), on
-      // 24 x 16-pixel tiles where the side allows (48 MFMAs per wave and K step instead of 32); A/B:
-      // debug 4096 = the 512 x 128 engine, 1 << 29 = the 16 x 16-pixel tiles
+      // 24 x 16-pixel tiles where the side allows (48 MFMAs per wave and K step instead of 32: 381 ->
+      // 369 us alone, profiles/r05am_cv3_24row/); debug 4096: the 512 x 128 engine
       const bool cv3 = a->a_mode == DP_A_CONV && a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 &&
                        a->in_h == a->in_w && a->out_h == a->in_h && a->out_w == a->in_w && a->in_w % 16 == 0 &&
                        a->in_c % 64 == 0 && a->head_corr && a->store_mode == DP_STORE_ROWS && a->c_dtype != DP_F32 &&
                        !a->R1 && !a->R2 && !a->gamma && !a->pos && !a->accumulate && !a->row_group && !(dbg & 4096);
       tile = !cv3 ? DP_TILE_BIG_512x128
-             : (a->in_w % 48 == 0 && !(dbg & (1 << 29))) ? DP_TILE_CV3_384x128 : DP_TILE_CV3_256x256;
+             : a->in_w % 48 == 0 ? DP_TILE_CV3_384x128 : DP_TILE_CV3_256x256;
     }
     else if (a->N % 256 != 0) tile = DP_TILE_BIG_256x128;
     else if (ws_ok && a->a_mode == DP_A_CONV && !(dbg & 32) && tiles256 < num_cus() &&
@@ -322,8 +322,8 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
     tile = DP_TILE_CV3_256x256;
   // ... and on 12 x 16-pixel tiles where those make whole rounds of workgroups and 16 x 16 ones do not
   // (the 384^2 maps: 768 tiles = 3 rounds instead of 576 = 2.25: 218 -> 187 us, 49.53 / 49.77 ->
-  // 50.00 / 49.99 fps same box, profiles/r05y_cv3_12row/; debug 1 << 30: off)
-  else if (a->tile == DP_TILE_AUTO && !(dbg & (1 << 16)) && !(dbg & (1 << 30)) && a->a_mode == DP_A_CONV &&
+  // 50.00 / 49.99 fps same box, profiles/r05y_cv3_12row/)
+  else if (a->tile == DP_TILE_AUTO && !(dbg & (1 << 16)) && a->a_mode == DP_A_CONV &&
            a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->in_w &&
            a->out_h == a->in_h && a->out_w == a->in_w && a->in_w % 16 == 0 && a->in_w % 12 == 0 &&
            a->in_c % 64 == 0 && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS && !a->row_group && !a->head_w &&
@@ -373,8 +373,6 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   p.ksplit = ksplit;
   p.kpart = ksplit > 1 ? (float*)((char*)a->workspace + SK_FLAG_BYTES) : nullptr;
   p.groups = 1;
-  p.stagger_wg = 0;
-  p.stagger_sleeps = 0;
   return 0;
 }
 }  // namespace
@@ -464,9 +462,7 @@ extern "C" int dp_gemm_grouped(const dp_gemm_args* a, int32_t groups, dp_stream_
   // work, so the side workgroups that hold CUs when a one-round patch-encoder launch starts free
   // them sooner (in-frame: 48.39 -> 48.91 fps, fc1 172 -> 165 us, profiles/r04h_side_tiles/; 64 x
   // 128: 48.47, profiles/r04i_side_tiles/; final round-5 tree: 49.81 / 50.38 / 50.23 / 49.98 vs
-  // 48.83 / 48.84 / 48.85 / 48.74 fps on 256 x 128, profiles/r05ay_side_tiles/).  Debug 1 << 26 (A/B):
-  // the 256 x 128 engine.
-  const int gt = (p.dbg & (1 << 26)) ? DP_TILE_BIG_256x128 : TILE_GRP_128x128;
-  return launch_part_big(p, gt, false, a->dtype == DP_BF16, s);
+  // 48.83 / 48.84 / 48.85 / 48.74 fps on 256 x 128, profiles/r05ay_side_tiles/).
+  return launch_part_big(p, TILE_GRP_128x128, false, a->dtype == DP_BF16, s);
 }
 

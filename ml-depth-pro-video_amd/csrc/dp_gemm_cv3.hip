@@ -408,7 +408,10 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
   p.tiles_n = p.N / bn;
   p.tiles_m = (p.M / (S * S)) * (S / th) * (S / CV_TW);
   dim3 grid(p.tiles_m * p.tiles_n);
-  const int abl = p.dbg & 2047;
+  // K-loop ablation / stamp variants (tools/cv3_stamps.py): only with debug bit 1 << 24 set, so that
+  // the planner's own debug bits (16, 32, 64, 1024, ...) never select one; an ablation
+  // value without a variant runs the normal kernel
+  const int abl = (p.dbg & (1 << 24)) ? p.dbg & 2047 : 0;
   if (th == 24) {   // 24 x 16-pixel tiles, 128 channels: 2 x 64 KiB patches + 2 x 16 KiB weight steps
     if (epi == CV_EPI_HPS) hipLaunchKernelGGL((gemm_cv3_kernel<K_, false, 128, CV_EPI_HPS, 0, 24>), grid, dim3(512), 0, s, p);
     else if (p.relu_a) hipLaunchKernelGGL((gemm_cv3_kernel<K_, true, 128, CV_EPI_BC, 0, 24>), grid, dim3(512), 0, s, p);
@@ -436,6 +439,7 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
       DP_CV3A(10) DP_CV3A(12) DP_CV3A(14) DP_CV3A(24) DP_CV3A(26) DP_CV3A(28) DP_CV3A(30) DP_CV3A(40) DP_CV3A(72)
       DP_CV3A(136) DP_CV3A(264) DP_CV3A(520) DP_CV3A(1032)
 #undef DP_CV3A
+      default: DP_CV3(256, CV_EPI_RES);
     }
   } else if (epi == CV_EPI_RES) DP_CV3(256, CV_EPI_RES);
   else if (epi == CV_EPI_HPS) DP_CV3(128, CV_EPI_HPS);

@@ -68,7 +68,6 @@ struct GemmP {
   float head_b;
   const float* head_corr;
   int tiles_n, tiles_m;
-  int stagger_wg, stagger_sleeps;   // 2-workgroup-per-CU engine: start stagger (debug 1 << 21)
   int dbg;  // ablation bits for tools/gemm_bench.py: 1 no stores, 2 no loads in loop, 4 no MFMA
   unsigned c_bytes;  // persistent engine: byte extent of C from p.C (buffer-store bound)
   // LayerNorm folded across the GEMM boundary (dp_gemm_args.ln_*; the 8-phase 320 x 256 engine)
@@ -1332,18 +1331,8 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
   for (int i = 0; i < FM; ++i)
     #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  // debug 1 << 17 (A/B): static priority -- waves 4-7 (the arbitration losers of each SIMD pair)
-  // at priority 1 for the whole loop instead of a raise / drop around every MFMA group
-  const bool sprio = p.dbg & (1 << 17);
-  if (sprio && wave_u >= 4) __builtin_amdgcn_s_setprio(1);
-  // two workgroups per CU (NW = 4): the second one of each CU (dispatch slots [ncu, 2 ncu)) starts
-  // about half a tile late, so one workgroup's epilogue runs beside the other's K loop instead of
-  // both reaching their epilogues together (A/B: debug 1 << 21)
-  if constexpr (NW == 4) {
-    if (p.stagger_wg && (int)blockIdx.x >= p.stagger_wg && (int)blockIdx.x < 2 * p.stagger_wg) {
-      for (int i = 0; i < p.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-  }
+  // (measured and rejected, round 2: static priority 1 for waves 4-7 instead of the raise / drop
+  // around every MFMA group, profiles/r02q_prio_band/)
 
   const int frow = lane & 15, fchunk = lane >> 4;
   constexpr int KS = BKT / 32;
@@ -1362,7 +1351,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
       uint4 afs[FM];
       #pragma unroll
       for (int i = 0; i < FM; ++i) afs[i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
-      if (!sprio) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
       #pragma unroll
       for (int i = 0; i < FM; ++i) {
         uint4 af = afs[i];
@@ -1370,7 +1359,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
         #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(bf[j], af, acc[i][j]);
       }
-      if (!sprio) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -1424,7 +1413,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
         fa[i] = *(const uint4*)(sa + lds_off_t<BKT>(wm * TM + i * 16 + frow, ks * 4 + fchunk));
     };
     auto mma = [&](const uint4 (&fa)[FM], const uint4 (&fb)[FN]) {
-      if (!sprio) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
       #pragma unroll
       for (int i = 0; i < FM; ++i) {
         uint4 a = fa[i];
@@ -1432,7 +1421,7 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
         #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = K_::mfma16(fb[j], a, acc[i][j]);
       }
-      if (!sprio) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
     };
     #pragma unroll
     for (int t = 0; t < NS - 1; ++t)
@@ -1491,7 +1480,6 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) gemm_big_kernel(cons
   }
 
   DP_STAMP(st2_);
-  if (sprio) __builtin_amdgcn_s_setprio(0);
   if (p.dbg & 1) {
     #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -1857,12 +1845,10 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
       for (int fn = 0; fn < 2; ++fn)
         bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((wn & 1) * 64 + qn * 32 + fn * 16 + frow, ks * 4 + fchunk));
   };
-  const bool sprio = p.dbg & (1 << 17);   // A/B: static priority for waves 4-7 (see gemm_big_kernel)
-  if (sprio && wave_u >= 4) __builtin_amdgcn_s_setprio(1);
   auto mma = [&](int qm, int qn) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (!sprio) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
@@ -1873,7 +1859,7 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
         for (int fn = 0; fn < 2; ++fn)
           acc[qm * 4 + fm][qn * 2 + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * 4 + fm][qn * 2 + fn]);
       }
-    if (!sprio) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   };
   auto bar = [&]() { asm volatile("s_barrier" ::: "memory"); };
 
@@ -1914,7 +1900,6 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph_kernel(const GemmP p) {
     bar();
   }
   if (wm == 0) bar();
-  if (sprio) __builtin_amdgcn_s_setprio(0);
   if (p.dbg & 1) {   // ablation (tools/gemm_bench.py --ablate): no epilogue
     #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -2233,7 +2218,12 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     const float* src;
     if ((lane & 16) == 0 && lane < 32) src = p.bias ? p.bias + n : (const float*)g_zero_page + 4 * l;
     else if (lane < 32) src = HG ? p.gamma + n : LNC ? p.ln_colsum + n : (const float*)g_zero_page + 4 * l;
-    else if (LNC && lane < 48) src = p.ln_rs + 2 * (tm * 256 + wm * TM + wn * 32 + 2 * (lane - 32));
+    else if (LNC && lane < 48) {
+      // rows past M (the last row tile) re-read the last even pair below M: the caller's buffer
+      // holds M rows (the planner refuses M < 2), and their values are never stored
+      const int row = tm * 256 + wm * TM + wn * 32 + 2 * (lane - 32);
+      src = p.ln_rs + 2 * (row + 1 < p.M ? row : ((p.M - 2) & ~1));
+    }
     else src = (const float*)g_zero_page + 4 * l;
     glds16(src, __builtin_amdgcn_readfirstlane(lds_addr(smem)) + RING + 8 * SLAB + (wave_u * 2 + par) * CST);
   };
@@ -2322,13 +2312,21 @@ __device__ __forceinline__ float2 ln_merge_row(const f32x4_t (&c)[4], float eps)
 // row tile adds one to the tile's counter; the last of the tiles_n arrivals merges the tile's rows
 // from ln_part_out (stored write-through, sc1, and drained before the add; read back with sc1
 // loads) into ln_rs_out and resets the counter for the next launch.  Replaces the persistent
-// consumer's pre-pass launch (ln_merge_kernel).  Guideline 16's sc1 hand-off: no fences.
+// consumer's pre-pass launch (ln_merge_kernel).  Guideline 16's sc1 hand-off, no fences: the
+// measured-valid form of MI355X_MICROARCH.md's hand-off table, row 1 (every byte stored sc1 and
+// drained by each storing wave before the barrier, ONE lane's agent-scope add to one counter, the
+// last adder's workgroup loading only with sc1 buffer loads after a barrier) -- an agent-scope
+// acq_rel add would also write back the XCD L2's dirty lines of the whole epilogue (~2-6 us per
+// workgroup at the end of every proj / fc2).  The signal fences keep the compiler from moving the
+// loads above the add (the barrier orders them too).
 __device__ __forceinline__ void ln_merge_last(const GemmP& p, int tile_m, int rows, char* smem, int tid) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's part stores (sc1) have landed
   __syncthreads();
   int* last = (int*)smem;
   if (tid == 0) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     const unsigned old = __hip_atomic_fetch_add(p.ln_cnt + tile_m, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     *last = old == (unsigned)(p.tiles_n - 1);
   }
   __syncthreads();
@@ -2418,22 +2416,17 @@ int launch_p8ph(const GemmP& p0, hipStream_t s) {
 // s+1 in phase 3 -- so each piece has 4+ phases to land and the count is 8 in steady state.
 // Dense A only; epilogues: the load-free MFMA-layout one (EACT = DP_ACT_*; 16-bit C) or the
 // fp32 residual-accumulate one (EACT = EPI_ACC + act).
-// TCH (split producer only; debug 1 << 28, measured and rejected): the K loop's first steps also
-// stream the wave's epilogue rows of the residual (hi 20 KiB + lo 10 KiB, 30 LDS-DMA pieces into a
-// dummy 1 KiB LDS slot, TT per step), so the epilogue's own reads of them would hit the caches
-// instead of HBM: proj 71.1 -> 76.9 us cold, fc2 155.9 -> 162.5, in-frame -0.8 fps
-// (profiles/r05av_residual_touch/) -- the extra DMA issue in the K loop costs more than it saves
-template <typename K_, int EACT, int LNM = 0, bool TCH = false>   // LNM: 1 folded-LN producer, 2 consumer, 3 (4) producer on hi + lo
+// (Measured and rejected, round 5: the K loop's first steps also streaming the wave's epilogue rows
+// of the residual into a dummy LDS slot, so the epilogue's reads would hit the caches: proj 71.1 ->
+// 76.9 us cold, fc2 155.9 -> 162.5, in-frame -0.8 fps, profiles/r05av_residual_touch/.)
+template <typename K_, int EACT, int LNM = 0>   // LNM: 1 folded-LN producer, 2 consumer, 3 (4) producer on hi + lo
 __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   constexpr int BM = 320;
   constexpr int A_BYTES = BM * 128, B_BYTES = 256 * 128, BUF = A_BYTES + B_BYTES;
   constexpr int FM = 5, FN = 8, TM = 80, TN = 128;
   constexpr int RING = 2 * BUF;                                   // 144 KiB
   constexpr int PF = 1, SLAB = PF * 16 * TN * 2;                  // epilogue_mfma slab per wave
-  constexpr int SMEM0 = RING > 8 * SLAB ? RING : 8 * SLAB;
-  constexpr int SMEM = TCH ? SMEM0 + 8 * 1024 : SMEM0;            // + the touch slots
-  static_assert(!TCH || LNM == 3, "touch: the split producer");
-  constexpr int TT = TCH ? 3 : 0, TSTEPS = 10;                    // touch pieces per step, steps
+  constexpr int SMEM = RING > 8 * SLAB ? RING : 8 * SLAB;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2464,22 +2457,6 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   };
   auto issueB = [&](int q, int t) {
     glds16(p.B + (boff + q * 32 * (int)p.ldb + t * 64), lds0 + (t & 1) * BUF + A_BYTES + (brow0 + q * 32) * 128);
-  };
-
-  // touch piece k of the wave's epilogue region (rows m0 + wm * 80 .., columns n0 + wn * 128 ..):
-  // k < 20: hi rows (k >> 2) * 16 + (k & 1) * 8 + lane / 8, column half (k >> 1) & 1; k >= 20: lo
-  // rows ((k - 20) >> 1) * 16 + lane / 4, column half (k - 20) & 1
-  auto touch = [&](int k) __attribute__((always_inline)) {
-    const uint32_t dst = lds0 + SMEM0 + wave_u * 1024;
-    const int mb = m0 + wm * TM, nb = n0 + wn * TN;
-    if (k < 20) {
-      const int m = min(mb + (k >> 2) * 16 + (k & 1) * 8 + (lane >> 3), p.M - 1);
-      glds16(p.ln_xb_out + (long long)m * p.ldc + nb + ((k >> 1) & 1) * 64 + (lane & 7) * 8, dst);
-    } else {
-      const int i = k - 20;
-      const int m = min(mb + (i >> 1) * 16 + (lane >> 2), p.M - 1);
-      glds16((const unsigned char*)p.ln_xl + (long long)m * p.ldc + nb + (i & 1) * 64 + (lane & 3) * 16, dst);
-    }
   };
 
   f32x4_t acc[FM][FN];
@@ -2536,39 +2513,27 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   for (int s = 0; s < KT; ++s) {
     const int buf = s & 1;
     const bool a1 = s + 1 < KT, a2 = s + 2 < KT;
-    // touch pieces of this step, issued after phase 0's wait: younger than everything phases 1-3
-    // retire (their counts + TT), older than what the next step's phase 0 retires
-    const bool tc = TCH && s < TSTEPS && s + 2 < KT;
     // phase 0: A fragments + B quarter 0; retire Bq1(s) (younger: 2 + 6 a1)
     readA(buf); readB(0, buf);
     if (a1) issueB(0, s + 1);
     if (a1) wait_vmcnt<8>(); else wait_vmcnt<2>();
-    if constexpr (TCH) {
-      if (tc) {
-        #pragma unroll
-        for (int k = 0; k < TT; ++k) touch(s * TT + k);
-      }
-    }
     bar(); mma(0); bar();
     // phase 1: retire Bq2(s) (younger: 1 + 7 a1)
     readB(1, buf);
     if (a1) issueB(1, s + 1);
-    if (tc) wait_vmcnt<8 + TT>();
-    else if (a1) wait_vmcnt<8>(); else wait_vmcnt<1>();
+    if (a1) wait_vmcnt<8>(); else wait_vmcnt<1>();
     bar(); mma(1); bar();
     // phase 2: A(s+2) pieces 0-2 into this step's buffer; retire Bq3(s) (younger: 5 a1 + 3 a2)
     readB(2, buf);
     if (a1) issueB(2, s + 1);
     if (a2) { issueA(0, s + 2); issueA(1, s + 2); issueA(2, s + 2); }
-    if (tc) wait_vmcnt<8 + TT>();
-    else if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<5>(); else wait_vmcnt<0>();
+    if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<5>(); else wait_vmcnt<0>();
     bar(); mma(2); bar();
     // phase 3: retire A(s+1) and Bq0(s+1) (younger: 3 + 5 a2)
     readB(3, buf);
     if (a1) issueB(3, s + 1);
     if (a2) { issueA(3, s + 2); issueA(4, s + 2); }
-    if (tc) wait_vmcnt<8 + TT>();
-    else if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<3>();
+    if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<3>();
     bar(); mma(3); bar();
   }
   if (wave < 4) bar();
@@ -2606,7 +2571,6 @@ int launch_8ph320(const GemmP& p0, hipStream_t s) {
     if (!p.ln_xb_out || p.act != DP_ACT_NONE) return DP_ERR_ARG;
     static_assert(8 * 13312 <= 2 * (320 * 128 + 256 * 128), "hi/lo staging fits the ring");
     if (p.dbg & (1 << 27)) hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 4>), grid, dim3(512), 0, s, p);
-    else if (p.dbg & (1 << 28)) hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3, true>), grid, dim3(512), 0, s, p);
     else hipLaunchKernelGGL((gemm_8ph320_kernel<K_, EPI_ACC + DP_ACT_NONE, 3>), grid, dim3(512), 0, s, p);
     DP_CHECK_LAUNCH();
     return 0;
@@ -3196,10 +3160,6 @@ int launch_dual(const GemmP& p0, bool conv, hipStream_t s) {
   p.tiles_n = (p.N + 127) / 128;
   p.tiles_m = (p.M + 255) / 256;
   dim3 grid(p.tiles_n * p.tiles_m);
-  if (p.dbg & (1 << 21)) {
-    p.stagger_wg = num_cus();
-    p.stagger_sleeps = (p.dbg >> 24) & 63;   // x 127 x 64 cycles
-  }
   if (conv && p.relu_a)
     hipLaunchKernelGGL((gemm_big_kernel<K_, 256, 128, 32, 3, false, true, true, 4>), grid, dim3(256), 0, s, p);
   else if (conv)

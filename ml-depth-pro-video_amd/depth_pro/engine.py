@@ -33,11 +33,11 @@ _ABLATE = set(filter(None, os.environ.get("DP_ABLATE", "").split(",")))
 
 
 def ln_fold_enabled() -> bool:
-    """Whether the patch encoder runs with its LayerNorms folded into qkv / fc1:
-    DP_LN_FOLD=1 (default), and no 'ln' / 'vitgemm' ablation -- those drop the standalone
-    LayerNorms / the ViT GEMMs, which only the unfolded path has as separate launches.
-    Read once at pack time: the packed set holds only the weights of the path chosen here."""
-    return os.environ.get("DP_LN_FOLD", "1") == "1" and not ({"ln", "vitgemm"} & _ABLATE)
+    """Whether the patch encoder runs with its LayerNorms folded into qkv / fc1: always,
+    except under the 'ln' / 'vitgemm' timing ablations -- those drop the standalone LayerNorms / the
+    ViT GEMMs, which only the unfolded path has as separate launches.  Read once at
+    pack time: the packed set holds only the weights of the path chosen here."""
+    return not ({"ln", "vitgemm"} & _ABLATE)
 
 
 NWIN = 35
@@ -246,15 +246,13 @@ class _ViTBuffers:
         # folded path: the residual stream between blocks is split, x = h (16 bits) + an 8-bit low
         # part xl (steps of ulp(h) / 256; the proj / fc2 epilogues read and update both, dp_gemm's
         # ln_xl); `x` (fp32) holds it only where an fp32 reader needs it (the patch embed's output, the
-        # hooks, the final norm).  DP_LN_SPLIT=0 (A/B only): the fp32 stream in `x`, read and written
-        # by every proj / fc2
-        split = ln_fold and os.environ.get("DP_LN_SPLIT", "1") == "1"
-        self.xl = torch.empty(rows, D, dtype=torch.int8, device=dev) if split else None
-        # split path (ABI 13): every row's (rstd, -rstd * mean), merged by the proj / fc2 producers'
-        # last workgroup per row tile for the qkv / fc1 consumers on the persistent engine
-        # (DP_LN_RS=0, A/B: the consumer's merge pre-pass from `part` instead)
-        self.rs = (torch.empty(rows, 2, dtype=torch.float32, device=dev)
-                   if split and os.environ.get("DP_LN_RS", "1") == "1" else None)
+        # hooks, the final norm)
+        self.xl = torch.empty(rows, D, dtype=torch.int8, device=dev) if ln_fold else None
+        # (ABI 13): every row's (rstd, -rstd * mean), merged by the proj / fc2 producers' last
+        # workgroup per row tile for the qkv / fc1 consumers on the persistent engine; padded to whole
+        # 256-row tiles, the rows the consumer's constant-slot DMA reads
+        self.rs = (torch.empty((rows + 255) // 256 * 256, 2, dtype=torch.float32, device=dev)
+                   if ln_fold else None)
         self.qkv = torch.empty(rows, 3 * D, dtype=dt, device=dev)
         self.a = torch.empty(rows, D, dtype=dt, device=dev)
         self.m = torch.empty(rows, MLP_DIM, dtype=dt, device=dev)
@@ -399,8 +397,8 @@ class Engine:
         # set was made for (DP_LN_FOLD / ablations at pack time, ln_fold_enabled)
         self.ln_fold = "encoder.patch_encoder.blocks.0.attn.qkv.fold.w" in packed
         if self.ln_fold != ln_fold_enabled():
-            raise DPError("packed weights were made for the other LayerNorm path (DP_LN_FOLD / DP_ABLATE "
-                          "differ from when they were packed)")
+            raise DPError("packed weights were made for the other LayerNorm path (DP_ABLATE differs from "
+                          "when they were packed)")
         self.vp = _ViTBuffers(NWIN * TOK, vdt, dev, dt, ln_fold=self.ln_fold)     # patch encoder (35 windows)
         # image + FOV encoders, run as one grouped ViT (rows 0..576 image, 577..1153 FOV)
         self.side_vits = ["encoder.image_encoder."] + (["fov.encoder.0."] if self.use_fov else [])
@@ -462,10 +460,6 @@ class Engine:
         # takes one exp2 per score (dp_attention_log2q)
         self.qkv_gamma = ops.log2q_gamma(HEADS, D // HEADS, dev)
         self.serial_side = False   # True: every launch on the current stream, in one order (profiling)
-        # side encoders gated block by block into chosen patch-encoder launches (_forward):
-        # DP_SIDE_GATE="release:join" points, e.g. "qkv:proj" or "fc2:fc1"; unset: free-running
-        g = os.environ.get("DP_SIDE_GATE", "")
-        self.side_gate = tuple(g.split(":")) if ":" in g else None
         # device status of the current frame: [error word of each workspace (forward's end),
         # non-finite output count (the infer epilogue)]
         self._wss = [self.ws_main, self.ws_dec]
@@ -475,30 +469,23 @@ class Engine:
         self._unreported: list = []       # finished bad frames owed to the next check_status
         self.last_status: Optional[FrameStatus] = None
         self.sync_check = os.environ.get("DP_CHECK_SYNC", "0") == "1"
-        self.dec_early = os.environ.get("DP_DEC_EARLY", "1") == "1"
-        # small-grid GEMMs of the main stream's post-encoder chain on the split-K engine: "4" the
-        # decoder's convs.4 (1024 -> 256 3x3 at 48^2: 9 tiles, 103 -> 41 us alone), "3" convs.3 (96^2,
-        # dec_c), "u" upsample2.0 (24^2 x 1024, 24 tiles), "f" fuse_lowres (48^2 x 1024, K 2048), "r" the
-        # fusions' 48^2 / 96^2 ResidualBlock convs (50 -> 36, 52 -> 43 us alone, but -0.2 fps in-frame); "0"
-        # the planner's choice.  Default "4": +0.23 / +0.12 / +0.09 fps in three same-box A/Bs, "4uf"
-        # +0.1 / -0.05, "34uf" -0.07 (profiles/r05ah_splitk_dec/); depth rel-L1 8.741e-4 -> 8.769e-4
-        self.splitk_dec = os.environ.get("DP_SPLITK_DEC", "4")
-        # the patch encoder's folded qkv on the persistent 8-phase engine (+ the LN merge pre-pass), as
-        # fc1: 948 tiles of 256 x 256 over 256 workgroups instead of 3 rounds of 320 x 256 tiles, each
-        # tile's epilogue under the next one's K loop: 48.41 / 48.27 -> 49.14 / 49.06 fps same box
-        # (profiles/r05i_qkv_p8ph/); DP_QKV_P8=0: the 8-phase 320 x 256 engine (A/B)
-        self.qkv_tile = DP_TILE_P8PH_256x256 if os.environ.get("DP_QKV_P8", "1") == "1" else 0
+        # the decoder's convs.4 (1024 -> 256 3x3 at 48^2: 9 tiles) on the split-K engine: 103 -> 41 us
+        # alone, +0.23 / +0.12 / +0.09 fps in three same-box A/Bs; convs.3, upsample2.0, fuse_lowres or
+        # the fusions' 48^2 / 96^2 ResidualBlock convs there too did not gain (profiles/r05ah_splitk_dec/)
+        # -- depth rel-L1 8.741e-4 -> 8.769e-4
+        # the patch encoder's folded qkv on the persistent 8-phase engine, as fc1: 948 tiles of 256 x 256
+        # over 256 workgroups instead of 3 rounds of 320 x 256 tiles, each tile's epilogue under the next
+        # one's K loop: 48.41 / 48.27 -> 49.14 / 49.06 fps same box (profiles/r05i_qkv_p8ph/)
+        self.qkv_tile = DP_TILE_P8PH_256x256
 
     # ------------------------------------------------------------------ ViT
-    def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, sync=None):
+    def _vit(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
         """timm forward_features (vit_factory.py:97-99 -> vision_transformer.py): patch embed + cls /
-        pos, 24 Blocks, final norm; `hooks[i]()` runs after block i (encoder.py:133-144).
-        `sync` (optional): sync(point, i) before block i's qkv / proj / fc1 / fc2 ("qkv", "proj",
-        "fc1", "fc2") -- where the side-encoder schedule gates the other stream (Engine._forward)."""
-        for _ in self._vit_steps(pres, buf, n_img, cols_off_rows, hooks, sync):
+        pos, 24 Blocks, final norm; `hooks[i]()` runs after block i (encoder.py:133-144)."""
+        for _ in self._vit_steps(pres, buf, n_img, cols_off_rows, hooks):
             pass
 
-    def _vit_steps(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None, sync=None):
+    def _vit_steps(self, pres, buf: _ViTBuffers, n_img: int, cols_off_rows: int, hooks=None):
         """`_vit` as a generator: yields after the embedding and after each Block (the final norm
         runs on the last step) -- lets a caller issue another stream's ViT block by block.
 
@@ -512,7 +499,6 @@ class Engine:
         # LayerNorm launches only (is the side chain's latency on the frame's critical path?)
         ln_on = "ln" not in _ABLATE and not (G > 1 and "sideln" in _ABLATE)
         gemm_on = "vitgemm" not in _ABLATE
-        sync = sync or (lambda what, i: None)
 
         def lin(A, key, C, N, K, a_rows=True, **kw):
             """The G problems' `key` Linear: A rows / C rows of problem g at g * M (A shared when
@@ -537,28 +523,24 @@ class Engine:
         for g, pre in enumerate(pres):
             ops.vit_cls_rows(buf.x[g * M:], P[pre + "cls"], P[pre + "pos"], n_img)
         if G == 1 and buf.part is not None:
-            yield from self._vit_blocks_folded(pres[0], buf, M, hooks, sync)
+            yield from self._vit_blocks_folded(pres[0], buf, M, hooks)
             return
         yield
         for i in range(DEPTH):
             b = f"blocks.{i}."
-            sync("qkv", i)
             if ln_on:
                 norm(b + "norm1", buf.h)
             if gemm_on:
                 lin(buf.h, b + "attn.qkv.weight", buf.qkv, 3 * D, D, bias=b + "attn.qkv.bias", gamma=self.qkv_gamma)
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, G * n_img, TOK, HEADS, D // HEADS, log2q=True)
-            sync("proj", i)
             if gemm_on:
                 lin(buf.a, b + "attn.proj.weight", buf.x, D, D, bias=b + "attn.proj.bias", gamma=b + "ls1.gamma",
                     accumulate=True)
             if ln_on:
                 norm(b + "norm2", buf.h)
-            sync("fc1", i)
             if gemm_on:
                 lin(buf.h, b + "mlp.fc1.weight", buf.m, MLP_DIM, D, bias=b + "mlp.fc1.bias", act=DP_ACT_GELU)
-            sync("fc2", i)
             if gemm_on:
                 lin(buf.m, b + "mlp.fc2.weight", buf.x, D, MLP_DIM, bias=b + "mlp.fc2.bias", gamma=b + "ls2.gamma",
                     accumulate=True)
@@ -568,52 +550,41 @@ class Engine:
                 norm("norm", buf.out)
             yield
 
-    def _vit_blocks_folded(self, pre: str, buf: _ViTBuffers, M: int, hooks=None, sync=None):
+    def _vit_blocks_folded(self, pre: str, buf: _ViTBuffers, M: int, hooks=None):
         """The 24 Blocks with norm1 / norm2 folded across the GEMM boundary (dp_gemm_args.ln_*):
         `h` carries the un-normalised residual rows in 16 bits and `part` their 128-column chunk
         statistics, written by the producer (block 0: dp_layernorm_stats; then every proj / fc2
-        epilogue beside its fp32 residual update); qkv / fc1 run on the folded weights
+        epilogue beside its split-residual update); qkv / fc1 run on the folded weights
         (ops.fold_layernorm) and apply LN's per-row mean / rstd in their epilogue.  Same
         arithmetic as LN -> Linear up to where the 16-bit rounding falls (x instead of LN(x);
         tools/ln_fold_emul.py: rel-L1 vs fp32 unchanged, 2.377e-3 vs 2.379e-3 bf16).  A generator
         like _vit_steps."""
         P = self.P
         n_img = M // TOK
-        sync = sync or (lambda what, i: None)
         # the stream enters as fp32 (patch embed + cls rows): split it into h + xl, with the stats
         ops.layernorm_stats(buf.x, buf.h, buf.part, M, D, xl=buf.xl)
-        split = buf.xl is not None
         yield
-        qkv_tile = self.qkv_tile if M > 4 * TOK else 0
+        qkv_tile = self.qkv_tile
         rs = buf.rs       # producer-merged row statistics (ABI 13), for the persistent consumers
         for i in range(DEPTH):
             b = f"{pre}blocks.{i}."
-            sync("qkv", i)
-            rs_q = rs if (i > 0 and qkv_tile) else None     # block 0: the stats pass wrote `part` only
+            rs_q = rs if i > 0 else None     # block 0: the stats pass wrote `part` only
             ops.gemm(buf.h, P[b + "attn.qkv.fold.w"], buf.qkv, M=M, N=3 * D, K=D, bias=P[b + "attn.qkv.fold.b"],
                      ln_in=(None if rs_q is not None else buf.part, P[b + "attn.qkv.fold.s"]), ln_rs_in=rs_q,
                      tile=qkv_tile)
             if "attn" not in _ABLATE:
                 ops.attention(buf.qkv, buf.a, n_img, TOK, HEADS, D // HEADS, log2q=True)
-            sync("proj", i)
-            ops.gemm(buf.a, P[b + "attn.proj.weight"], None if split else buf.x, M=M, N=D, K=D,
+            ops.gemm(buf.a, P[b + "attn.proj.weight"], None, M=M, N=D, K=D,
                      bias=P[b + "attn.proj.bias"], gamma=P[b + "ls1.gamma"], accumulate=True,
                      ln_out=(buf.h, buf.part), ln_xl=buf.xl, ln_rs_out=rs)
-            sync("fc1", i)
             ops.gemm(buf.h, P[b + "mlp.fc1.fold.w"], buf.m, M=M, N=MLP_DIM, K=D, bias=P[b + "mlp.fc1.fold.b"],
-                     act=DP_ACT_GELU, ln_in=(None if rs is not None else buf.part, P[b + "mlp.fc1.fold.s"]),
-                     ln_rs_in=rs)
+                     act=DP_ACT_GELU, ln_in=(None, P[b + "mlp.fc1.fold.s"]), ln_rs_in=rs)
             last = i == DEPTH - 1    # the final norm reads x itself
             # fp32 rows only where they are read: the hooks (merge_windows) and the final norm
-            need_x = last or bool(hooks and i in hooks) or not split
-            sync("fc2", i)
-            if split:
-                ln_out = (buf.h, None if last else buf.part)
-            else:
-                ln_out = None if last else (buf.h, buf.part)
+            need_x = last or bool(hooks and i in hooks)
             ops.gemm(buf.m, P[b + "mlp.fc2.weight"], buf.x if need_x else None, M=M, N=D, K=MLP_DIM,
                      bias=P[b + "mlp.fc2.bias"], gamma=P[b + "ls2.gamma"], accumulate=True,
-                     ln_out=ln_out, ln_xl=buf.xl, ln_rs_out=None if last or not qkv_tile else rs)
+                     ln_out=(buf.h, None if last else buf.part), ln_xl=buf.xl, ln_rs_out=None if last else rs)
             if hooks and i in hooks:
                 hooks[i]()
             if last:
@@ -624,8 +595,6 @@ class Engine:
     def _conv3(self, x, s_in, cin, w, out, cout, bias=None, relu_a=False, act=0, R1=None, R2=None,
                stride=1, border_corr=None, tile=0):
         s_out = (s_in + 2 - 3) // stride + 1
-        if not tile and "r" in self.splitk_dec and s_in in (48, 96) and stride == 1 and cin == 256 and cout == 256:
-            tile = DP_TILE_SPLITK_256x256     # the fusions' 48^2 / 96^2 ResidualBlock convs (main stream)
         ops.gemm(x, w, out, M=s_out * s_out, N=cout, K=9 * cin,
                  conv=dict(in_h=s_in, in_w=s_in, in_c=cin, k=3, stride=stride, pad=1, out_h=s_out, out_w=s_out),
                  relu_a=relu_a, bias=bias, act=act, R1=R1, ldr1=cout, R2=R2, ldr2=cout, ldc=cout,
@@ -732,35 +701,12 @@ class Engine:
 
         # pyramid + 35 windows + patch-embed im2col (encoder.py:151-263)
         ops.patchify_pyramid(self.x0, self.cols)
-        # image and FOV encoders (one grouped ViT, M = 2 x 577 rows) beside the patch encoder:
-        # free-running on the side stream, or (side_gate = (R, J)) side block k released when the
-        # patch encoder reaches point R of its block k and joined before the next point J, so that
-        # side workgroups land only in chosen launches (points: qkv < proj < fc1 < fc2 of a block)
-        gate = self.side_gate if side_ok and not serial else None
-        sync = None
-        if side_ok and not gate:
+        # image and FOV encoders (one grouped ViT, M = 2 x 577 rows) beside the patch encoder, free-running
+        # on the side stream (measured and rejected, round 4: side blocks gated into chosen patch-encoder
+        # launches, -1.1 to -2.6 fps, profiles/r04e_ab/, r04f_ab/)
+        if side_ok:
             with self._on(self.side):
                 self._side_encoders()
-        elif gate:
-            steps = self._side_steps()
-            with self._on(self.side):
-                next(steps)                         # the side embedding (after patchify)
-            order = ("qkv", "proj", "fc1", "fc2")
-            rel, join = gate
-            pending = []
-
-            def sync(what, i):
-                if pending and what == join and (i > pending[0][0] or order.index(join) > order.index(rel)):
-                    main.wait_event(pending.pop(0)[1])
-                if what == rel:                     # main has issued everything before this point
-                    ev = torch.cuda.Event()
-                    ev.record(main)
-                    self.side.wait_event(ev)
-                    with _StreamCtx(self.side):
-                        next(steps)                 # side block i
-                    done = torch.cuda.Event()
-                    done.record(self.side)
-                    pending.append((i, done))
         # patch encoder; hooks after blocks 5 / 11 (encoder.py:133-144, 267-288)
         vp = self.vp
         ev = {}
@@ -783,11 +729,7 @@ class Engine:
         # blocks 6..23: 47.88 / 47.76 vs 48.17 / 48.07 fps, profiles/r05g_lat_early/)
         hooks = {5: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat0),
                  11: lambda: ops.merge_windows(vp.x, 0, 5, 3, self.lat1)}
-        self._vit(["encoder.patch_encoder."], vp, NWIN, 0, hooks, sync)
-        if gate:
-            with _StreamCtx(self.side):
-                for _ in steps:                     # the side encoders' tail (lowres upsample, FOV Linear)
-                    pass
+        self._vit(["encoder.patch_encoder."], vp, NWIN, 0, hooks)
         ops.merge_windows(vp.out, 0, 5, 3, self.f0)
         ops.merge_windows(vp.out, 25, 3, 6, self.f1)
         ops.merge_windows(vp.out, 34, 1, 0, self.f2)
@@ -795,12 +737,12 @@ class Engine:
         # project / upsample (encoder.py:314-324): the latent and f0 / f1 chains (small grids) beside
         # the main stream's f2 chain -> fuse_lowres -> convs.4, in the order the decoder's
         # projections need their outputs
-        # DP_DEC_EARLY=1 (default): fusion 0's resnet1 first conv (768^2; needs only enc0, its output
-        # in dec[768]["c"], unused at 768^2) on dec_c right after the lat0 chain's last deconv, beside
-        # fusion 1 (384^2) instead of after it: 48.17 / 48.19 -> 48.60 / 48.74 fps same box
-        # (profiles/r05f_dec_early/); on dec_a with the whole lat0 chain, beside fuse_lowres and
-        # fusions 4..1, it was slower (47.61 / 47.48): the small-grid fusions then wait for CUs
-        early = self.dec_early and "decoder" not in _ABLATE
+        # fusion 0's resnet1 first conv (768^2; needs only enc0, its output in dec[768]["c"], unused at
+        # 768^2) on dec_c right after the lat0 chain's last deconv, beside fusion 1 (384^2) instead of
+        # after it: 48.17 / 48.19 -> 48.60 / 48.74 fps same box (profiles/r05f_dec_early/); on dec_a with
+        # the whole lat0 chain, beside fuse_lowres and fusions 4..1, it was slower (47.61 / 47.48): the
+        # small-grid fusions then wait for CUs
+        early = "decoder" not in _ABLATE
         t1 = self.dec[768]["c"] if early else None
         lat0_chain()
         with self._on(self.dec_b):
@@ -812,16 +754,14 @@ class Engine:
             ev["enc2"] = mark(self.dec_b)
         lat1_chain()
         sk = DP_TILE_SPLITK_256x256
-        ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D,
-                 tile=sk if "u" in self.splitk_dec else 0)
+        ops.gemm(self.f2, P[e + "upsample2.0"], self.t24_1024, M=24 * 24, N=D, K=D)
         self._deconv(self.t24_1024, 24, D, P[e + "upsample2.1"], self.cat, D, ldc=2 * D)
         if not serial:
             main.wait_stream(self.side)  # join: the image-encoder half of `cat`
-        ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"],
-                 tile=sk if "f" in self.splitk_dec else 0)
+        ops.gemm(self.cat, P[e + "fuse_lowres.w"], self.enc4, M=48 * 48, N=D, K=2 * D, bias=P[e + "fuse_lowres.b"])
         # decoder (decoder.py:74-93)
         self._conv3(self.enc4, 48, D, P["decoder.convs.4"], self.low, 256,
-                    tile=sk if "4" in self.splitk_dec else 0)
+                    tile=sk)
         # dec_c (after convs.4, the main stream's last stream-K launch before fusion 1's deconv, which
         # waits for convs.1 -- so dec_c's stream-K launches never overlap the main stream's):
         # convs.3 / .2 / .1 in the order the fusions need them, the lat0 chain's 384^2 -> 768^2
@@ -831,8 +771,7 @@ class Engine:
                                       (1, (self.enc1, 384, 256))):
                 if not serial:
                     self.dec_c.wait_event(ev[f"enc{i}"])
-                self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256,
-                            tile=DP_TILE_SPLITK_256x256 if str(i) in self.splitk_dec and i >= 3 else 0)
+                self._conv3(enc, s_, cin, P[f"decoder.convs.{i}"], self.dec[s_]["c"], 256)
                 ev[f"c{i}"] = mark(self.dec_c)
             if not serial:
                 self.dec_c.wait_event(ev["lat0pre"])

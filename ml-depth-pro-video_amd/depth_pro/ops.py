@@ -33,6 +33,10 @@ def dtype_code(dt: torch.dtype) -> int:
 # Optional per-launch timing (bench.py's roofline leg): list of (kind, flops, shape, dtype, ev0, ev1, stream).
 _PROF: Optional[list] = None
 _PROF_T0: Optional[torch.cuda.Event] = None
+# While profiling: what selects a GEMM's kernel instantiation beyond its tile, per (kind, shape, dtype)
+# -- the epilogue activation and whether it is a folded-LN consumer / a deconv store (bench.py names
+# the dominant launch's rocprof kernel from it instead of guessing from the shape)
+PROF_GEMM_META: dict = {}
 
 
 def profile_begin() -> None:
@@ -215,6 +219,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
     _check_gemm_extents(A, B, C if a.C else None, a, A_off, C_off, conv, deconv, head_w is not None,
                         head_corr is not None, B_off)
     kind = "gemm_conv" if conv is not None else ("gemm_deconv" if deconv is not None else "gemm")
+    if _PROF is not None:
+        PROF_GEMM_META[(kind, (M, N, K), B.dtype)] = {"act": int(act), "ln_consumer": bool(a.ln_colsum),
+                                                     "deconv": deconv is not None}
     with _Timed(kind, 2.0 * M * N * K, (M, N, K), B.dtype):
         check(_lib.load().dp_gemm(ctypes.byref(a), _stream(B)), "dp_gemm")
 

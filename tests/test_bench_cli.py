@@ -42,8 +42,7 @@ def test_launcher_world_size_must_match_gpus():
     assert line.get("value") is None and "launcher started 2" in line["error"]
 
 
-@pytest.mark.parametrize("env", [{"DP_ABLATE": "side"}, {"DP_GEMM_DEBUG": "8192"}, {"DP_SIDE_GATE": "fc2:fc1"},
-                                 {"DP_LN_FOLD": "0"}])
+@pytest.mark.parametrize("env", [{"DP_ABLATE": "side"}, {"DP_GEMM_DEBUG": "8192"}])
 def test_ablation_or_debug_switch_refused(env):
     """DP_ABLATE / DP_GEMM_DEBUG make the frame invalid or change its schedule: no value
     (exit 3) unless the run is an explicit --ab timing run."""

@@ -1074,8 +1074,7 @@ def test_layernorm_stats_split_residual(cuda, dt):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("M,K,fp32_out,with_part,dbg", [(20195, 1024, False, True, 0), (577, 4096, True, True, 0),
-                                                         (20195, 4096, True, False, 0), (20195, 1024, True, True, 1 << 27),
-                                                         (20195, 1024, False, True, 1 << 28)])
+                                                         (20195, 4096, True, False, 0), (20195, 1024, True, True, 1 << 27)])
 def test_gemm_8ph320_split_residual_producer(cuda, dt, M, K, fp32_out, with_part, dbg):
     """Folded-LN producer on the split residual (ABI 12, dp_gemm ln_xl; the ViT proj / fc2): with the
     stream given as (hi, int8 lo), the new rows are bit-identical to the fp32 producer's on C =

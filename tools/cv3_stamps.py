@@ -43,7 +43,9 @@ def main():
         ops.gemm(A, B, C, M=S * S, N=N, K=9 * cin, conv=conv, bias=bias, relu_a=True, act=0 if R1 is not None else 1,
                  R1=R1, ldr1=N if R1 is not None else 0, tile=DP_TILE_CV3_256x256 if args.th == 16 else DP_TILE_CV3_192x256)
 
-    for flags, lab in (((0, "plain"),) if not args.abl else ()) + ((8 | args.abl, f"stamped (bits {8 | args.abl})"),):
+    # (the cv3 ablation / stamp variants are selected only with debug bit 1 << 24, dp_gemm_cv3.hip)
+    for flags, lab in (((0, "plain"),) if not args.abl else ()) + (((1 << 24) | 8 | args.abl,
+                                                                   f"stamped (bits {8 | args.abl})"),):
         lib.dp_gemm_debug_flags(flags)
         run()
         torch.cuda.synchronize()

@@ -17,7 +17,6 @@ def main():
     packed = pack_weights(synthetic_state_dict(0), dev, code)
     model = DepthPro.from_packed(packed, dev, code)
     eng = model.engine()
-    print("dec_early", eng.dec_early, flush=True)
     eng.forward()
     torch.cuda.synchronize()
     print("eager ok", flush=True)
