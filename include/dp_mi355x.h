@@ -154,7 +154,8 @@ typedef struct dp_gemm_args {
    * ln_part_out set, a workspace), the last workgroup to finish each row tile merges the tile's
    * rows' 8 chunk statistics into ln_rs_out[m] = (rstd, -rstd * mean) (eps ln_eps; the arithmetic
    * of the pre-pass, bit for bit); a consumer on the persistent 8-phase engine takes ln_rs_in =
-   * that array instead of ln_part_in (no pre-pass launch, no workspace needed). */
+   * that array instead of ln_part_in (no pre-pass launch, no workspace needed).  ln_rs_in holds
+   * M rounded up to an even number of rows (its reads go in row pairs). */
   float* ln_rs_out;
   const float* ln_rs_in;
 } dp_gemm_args;

@@ -133,7 +133,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
                        !(a->workspace && a->workspace_bytes >= dp_gemm_workspace_size()) ||
                        (a->M + 319) / 320 > 1023 - LN_CNT_WORD))
     return DP_ERR_ARG;
-  if (a->ln_rs_in && ((a->tile != DP_TILE_AUTO && a->tile != DP_TILE_P8PH_256x256) || a->M < 2)) return DP_ERR_ARG;
+  if (a->ln_rs_in && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_P8PH_256x256) return DP_ERR_ARG;
   if ((lnp || lnc) && a->tile != DP_TILE_AUTO && a->tile != DP_TILE_8PH_320x256 &&
       !(lnc && a->tile == DP_TILE_P8PH_256x256))   // (a consumer may ask for the persistent engine)
     return DP_ERR_ARG;

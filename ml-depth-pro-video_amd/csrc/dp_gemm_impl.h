@@ -2219,10 +2219,10 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     if ((lane & 16) == 0 && lane < 32) src = p.bias ? p.bias + n : (const float*)g_zero_page + 4 * l;
     else if (lane < 32) src = HG ? p.gamma + n : LNC ? p.ln_colsum + n : (const float*)g_zero_page + 4 * l;
     else if (LNC && lane < 48) {
-      // rows past M (the last row tile) re-read the last even pair below M: the caller's buffer
-      // holds M rows (the planner refuses M < 2), and their values are never stored
+      // rows past M (the last row tile) re-read the pair holding row M - 1, whose values they
+      // never store: the caller's buffer holds M rounded up to even rows
       const int row = tm * 256 + wm * TM + wn * 32 + 2 * (lane - 32);
-      src = p.ln_rs + 2 * (row + 1 < p.M ? row : ((p.M - 2) & ~1));
+      src = p.ln_rs + 2 * (row < p.M ? row : ((p.M - 1) & ~1));
     }
     else src = (const float*)g_zero_page + 4 * l;
     glds16(src, __builtin_amdgcn_readfirstlane(lds_addr(smem)) + RING + 8 * SLAB + (wave_u * 2 + par) * CST);

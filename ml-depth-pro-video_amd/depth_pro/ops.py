@@ -206,7 +206,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, *, M: int, N: int, K
         part, colsum = ln_in
         if (part is None) == (ln_rs_in is None) or colsum.numel() < N or colsum.dtype != torch.float32 or \
                 (part is not None and part.numel() < M * (K // 128) * 2) or \
-                (ln_rs_in is not None and (ln_rs_in.numel() < 2 * M or ln_rs_in.dtype != torch.float32)):
+                (ln_rs_in is not None and (ln_rs_in.numel() < 2 * (M + (M & 1)) or ln_rs_in.dtype != torch.float32)):
             raise _lib.DPError("dp_gemm: ln_in buffers too small or of the wrong type")
         a.ln_part_in, a.ln_colsum, a.ln_eps = _p(part), colsum.data_ptr(), float(ln_eps)
         a.ln_rs_in = _p(ln_rs_in)

@@ -379,6 +379,24 @@ def test_resize_and_infer_epilogue(cuda, HW):
                                rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mode", ["bilinear", "bicubic"])
+def test_resize_same_size_is_a_copy(cuda, dt, mode):
+    """dp_resize at input size == output size (the infer prologue of a 1536^2 frame) copies, as
+    F.interpolate's same-size fast path does: bit-exact, non-finite inputs included."""
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(3, 1536, 1536, generator=g)
+    x[0, 5, 7], x[1, 100, 1535], x[2, 1535, 0] = float("nan"), float("inf"), -float("inf")
+    x = x.to(dt)
+    out = torch.full((3, 1536, 1536), 7.0, device=cuda)
+    ops.resize(x.to(cuda), out, mode)
+    ref = F.interpolate(x.float()[None], size=(1536, 1536), mode=mode, align_corners=False)[0]
+    assert torch.equal(out.cpu().nan_to_num(123.0), ref.nan_to_num(123.0))
+    odd = torch.randn(3, 37, 53, generator=g)          # a ragged size, fp32 (the scalar tail)
+    o2 = torch.empty(3, 37, 53, device=cuda)
+    ops.resize(odd.to(cuda), o2, mode)
+    assert torch.equal(o2.cpu(), odd)
+
 @pytest.mark.parametrize("HW", [(1536, 1536), (1080, 1920), (500, 333), (3000, 2000)])
 def test_resize_and_infer_epilogue_bicubic(cuda, HW):
     """interpolation_mode="bicubic" (reference depth_pro.py:273-291 passes it to both
