@@ -316,7 +316,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
   if (a->tile == DP_TILE_AUTO && !(dbg & (1 << 16)) && a->a_mode == DP_A_CONV && a->k_h == 3 && a->k_w == 3 &&
       a->stride == 1 && a->pad == 1 && a->in_h == a->in_w && a->out_h == a->in_h && a->out_w == a->in_w &&
       a->in_w % 16 == 0 && a->in_c % 64 == 0 && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS &&
-      !a->row_group && !a->head_w && !a->head_corr && (long long)a->M * a->in_c < (1LL << 31) && off32 &&
+      !a->row_group && !a->head_w && !a->head_corr && (long long)a->M * a->in_c < (1LL << 30) && off32 &&
       a->c_dtype != DP_F32 && !a->gamma && !a->pos && !a->accumulate && a->act != DP_ACT_GELU &&
       (long long)(a->M / 256) * (a->N / 256) >= 4LL * num_cus())   // many rounds (the 768^2 maps; 384^2: 201 vs 185 us)
     tile = DP_TILE_CV3_256x256;
@@ -327,7 +327,7 @@ int gemm_plan(const dp_gemm_args* a, GemmP& p, int& tile) {
            a->k_h == 3 && a->k_w == 3 && a->stride == 1 && a->pad == 1 && a->in_h == a->in_w &&
            a->out_h == a->in_h && a->out_w == a->in_w && a->in_w % 16 == 0 && a->in_w % 12 == 0 &&
            a->in_c % 64 == 0 && a->N % 256 == 0 && a->store_mode == DP_STORE_ROWS && !a->row_group && !a->head_w &&
-           !a->head_corr && (long long)a->M * a->in_c < (1LL << 31) && off32 && a->c_dtype != DP_F32 && !a->gamma &&
+           !a->head_corr && (long long)a->M * a->in_c < (1LL << 30) && off32 && a->c_dtype != DP_F32 && !a->gamma &&
            !a->pos && !a->accumulate && a->act != DP_ACT_GELU) {
     const long long t12 = (long long)(a->M / ((long long)a->in_w * a->in_w)) * (a->in_w / 12) * (a->in_w / 16) * (a->N / 256);
     const long long ncu = num_cus();

@@ -31,8 +31,17 @@ constexpr int CV_PW = CV_TW + 2;              // patch width
 template <int TH> struct CvGeo {
   static constexpr int PIX = (TH + 2) * CV_PW;              // patch pixels (324 / 252 / 468)
   static constexpr int PPW = (PIX * 8 + 511) / 512;          // LDS-DMA pieces per wave (6 / 4 / 8)
-  static constexpr int PATCH_B = 8 * PPW * 1024;             // bytes per patch buffer
+  static constexpr int PATCH_B = 8 * PPW * 1024;             // bytes the DMA writes per patch buffer
   static constexpr int FM = TH / 2, HQ = FM / 2;             // fragment rows per wave / per phase
+  // TIGHT (TH 16 / 12): the two patch buffers PSTRIDE apart = the patch rounded up to whole 1-KiB
+  // pieces (41 / 32 KiB), the dummy pieces past it written to a 1-KiB trash slot, so that every
+  // fragment read of the second buffer is still base register + a 16-bit immediate (< 64 KiB);
+  // TH 24 (59 KiB patches) moves its address registers by +- PATCH_B per channel block instead
+  static constexpr int NREAL = (PIX + 7) / 8;                  // pieces holding patch pixels
+  static constexpr bool TIGHT = NREAL * 1024 + ((FM + 1) * CV_PW + 2) * 128 < 65536;
+  static constexpr int PSTRIDE = TIGHT ? NREAL * 1024 : PATCH_B;
+  static constexpr int TRASH = 2 * PSTRIDE;                    // (TIGHT) dummy pieces
+  static constexpr int WOFF = TIGHT ? 2 * PSTRIDE + 1024 : 2 * PATCH_B;   // weight ring
 };
 
 // BN: output channels per tile (256: the ResidualBlock convs; 128: the head convs).  EPI:
@@ -55,13 +64,15 @@ template <typename K_, bool RELU, int BN, int EPI, int ABL = 0, int TH = 16>
 __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   using G = CvGeo<TH>;
   constexpr int FM = G::FM, HQ = G::HQ, PPW = G::PPW, CV_PATCH_B = G::PATCH_B, CV_PIX = G::PIX;
+  constexpr bool TIGHT = G::TIGHT;
+  constexpr int PSTRIDE = G::PSTRIDE, WOFF = G::WOFF;
   constexpr int TN = BN / 4, FN = TN / 16, QF = FN / 2;          // wave tile 16 FM x TN
   static_assert(TH == 16 || TH == 12 || (TH == 24 && BN == 128), "tile rows");
   constexpr int NBH = BN / 128;                                  // weight halves per K step
   constexpr int B_B = BN * 128;                                  // bytes per weight K step
   static_assert(EPI != CV_EPI_RES || BN == 256, "residual epilogue: BN 256");
   static_assert(EPI != CV_EPI_HPS || BN == 128, "head epilogue: one parity (32 columns) per wave");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * CV_PATCH_B + 2 * B_B];
+  __shared__ __attribute__((aligned(1024))) char smem[WOFF + 2 * B_B];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = tid >> 6;
@@ -80,45 +91,49 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   const int cin = p.in_c, CB = cin / 64;
   const int KT = CB * 9;
 
-  // patch pieces of this lane: element offset of its 16-B chunk (channel block 0), or -1 when
-  // the pixel is in the zero padding or past the patch
-  int poff[PPW];
-  #pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int c = (wave * PPW + i) * 64 + lane;   // chunk index in the patch image
+  // patch pieces of this lane: byte offset of its 16-B chunk (channel block 0) in the input map, or
+  // CV_PAD when the pixel is in the zero padding or past the patch (read as zeros: past the end of
+  // the buffer resource, glds16b; host: the map is < 2 GiB)
+  // Computed where the pieces are issued (once per channel block) from a laundered lane index, so
+  // that the compiler does not hoist the PPW offsets out of the K loop (they would hold PPW VGPRs
+  // through it, where the unrolled loop's address bases need them).
+  constexpr uint32_t CV_PAD = 0x80000000u;
+  auto patch_off = [&](int i, int c0) __attribute__((always_inline)) {
+    const int c = c0 + i * 64;                    // chunk index in the patch image
     const int P = c >> 3, slot = c & 7;
-    int off = -1;
+    uint32_t off = CV_PAD;
     if (P < CV_PIX) {
       const int pr = P / CV_PW, pc = P - pr * CV_PW;
       const int iy = y0 - 1 + pr, ix = x0 - 1 + pc;
       if ((unsigned)iy < (unsigned)S && (unsigned)ix < (unsigned)S)
-        off = ((img * S + iy) * S + ix) * cin + ((slot ^ (P & 7)) << 3);
+        off = 2u * (uint32_t)(((img * S + iy) * S + ix) * cin + ((slot ^ (P & 7)) << 3));
     }
-    poff[i] = off;
-  }
+    return off;
+  };
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  const u32x4_t a_rs = raw_rsrc(p.A, (uint32_t)((long long)p.M * cin * 2));
 
   // weight K step t in the 8-phase layout (gemm_8ph_kernel): NBH halves of 128 rows (output
   // channels), 16 KiB each; half h rows h*128 + i*64 + wave*8 + lane/8, chunk swizzled on the source
   constexpr int HALF = 128 * 128;
   const int prow = wave * 8 + (lane >> 3);
   const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
-  int boff[NBH][2];
-  #pragma unroll
-  for (int h = 0; h < NBH; ++h)
-    #pragma unroll
-    for (int i = 0; i < 2; ++i) boff[h][i] = (n0 + h * 128 + i * 64 + prow) * (int)p.ldb + pchunk * 8;
+  // byte offset of this lane's weight row (prow) from the piece's scalar base p.B + (h 128 + i 64)
+  // ldb + 64 t (host: N * ldb < 2^31): one VGPR, the rest wave-uniform
+  const uint32_t boff = 2u * (uint32_t)((n0 + prow) * (int)p.ldb + pchunk * 8);
   auto issue_b = [&](int h, int t) {   // half h of weight step t -> stage t & 1
-    const uint32_t dst = lds0 + 2 * CV_PATCH_B + (t & 1) * B_B + h * HALF + wave_u * 1024;
+    const uint32_t dst = lds0 + WOFF + (t & 1) * B_B + h * HALF + wave_u * 1024;
     #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(p.B + (boff[h][i] + t * 64), dst + i * 8192);
+    for (int i = 0; i < 2; ++i) glds16s(boff, p.B + (long long)(h * 128 + i * 64) * p.ldb + 64 * t, dst + i * 8192);
   };
   auto issue_patch3 = [&](int cb, int buf, int i0) {   // half of the wave's PPW patch pieces
-    const uint32_t dst = lds0 + buf * CV_PATCH_B + wave_u * PPW * 1024;
+    int c0 = wave * PPW * 64 + lane;              // the lane's chunk of piece 0
+    asm volatile("" : "+v"(c0));
     #pragma unroll
     for (int i = i0; i < i0 + PPW / 2; ++i) {
-      const void* src = poff[i] >= 0 ? (const void*)(p.A + (poff[i] + cb * 64)) : (const void*)g_zero_page;
-      glds16(src, dst + i * 1024);
+      const int j = wave_u * PPW + i;                   // piece index in the patch image
+      const uint32_t dst = lds0 + ((!TIGHT || j < G::NREAL) ? buf * PSTRIDE + j * 1024 : G::TRASH);
+      glds16b(patch_off(i, c0) + cb * 128, a_rs, dst);
     }
   };
 
@@ -129,15 +144,37 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int frow = lane & 15, fchunk = lane >> 4;
   uint4 af[2][HQ], bf[2][2][QF];
-  // half qm of the wave tile = output pixel rows wm*FM + qm*HQ .. +HQ-1; tap (ky, kx) of patch buffer pb
-  auto readA = [&](int qm, int pb, int ky, int kx) {
-    const char* pa = smem + pb * CV_PATCH_B;
+  // Fragment addresses as per-lane bases + compile-time offsets (the K loop below is unrolled over
+  // the 9 taps and the 2 weight stages): patch pixel P = PB + c with PB = wm FM 18 + frow (this lane)
+  // and c = (qm HQ + fm + ky) 18 + kx (constant), whose 16-B chunk is stored at slot chunk ^ (P & 7)
+  // = chunk ^ ((PB + (c & 7)) & 7) -- so 8 x 2 bases (c & 7, ks), each + c * 128 as the ds_read
+  // immediate (+ PSTRIDE for the second patch buffer when TIGHT; else the bases move by
+  // +- CV_PATCH_B per channel block).
+  // B: row r = wn TN + qn TN / 2 + fn 16 + frow, r & 7 = frow & 7 (TN / 2 a multiple of 16), so one
+  // base per ks + a constant.  (Was: ~80 VALU of address arithmetic per K step.)
+  typedef __attribute__((address_space(3))) const char lds_c;
+  typedef __attribute__((address_space(3))) const u32x4_t lds_u4;   // (16-B alignment known: one ds_read_b128)
+  uint32_t abase[8][2], bbase[2];
+  {
+    const int PB = wm * FM * CV_PW + frow;
+    #pragma unroll
+    for (int v = 0; v < 8; ++v)
+      #pragma unroll
+      for (int ks = 0; ks < 2; ++ks) abase[v][ks] = lds0 + PB * 128 + (((ks * 4 + fchunk) ^ ((PB + v) & 7)) << 4);
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      bbase[ks] = lds0 + WOFF + (wn * TN + frow) * 128 + (((ks * 4 + fchunk) ^ (frow & 7)) << 4);
+  }
+  // half qm of the wave tile = output pixel rows wm*FM + qm*HQ .. +HQ-1; tap (ky, kx) of the current
+  // patch buffer (all four compile-time constants in the K loop)
+  auto readA = [&](int qm, int ky, int kx, int pb) __attribute__((always_inline)) {
+    const int boff_ = TIGHT ? pb * PSTRIDE : 0;
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
       for (int fm = 0; fm < HQ; ++fm) {
-        const int P = (wm * FM + qm * HQ + fm + ky) * CV_PW + frow + kx;
-        af[ks][fm] = *(const uint4*)(pa + P * 128 + (((ks * 4 + fchunk) ^ (P & 7)) << 4));
+        const int c = (qm * HQ + fm + ky) * CV_PW + kx;
+        af[ks][fm] = __builtin_bit_cast(uint4, *(lds_u4*)((lds_c*)(uintptr_t)abase[c & 7][ks] + boff_ + c * 128));
       }
     if constexpr (RELU && (ABL & 32)) {   // the ReLU prologue by the reading wave, before the barrier
       #pragma unroll
@@ -147,14 +184,12 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  auto readB = [&](int qn, int st) {   // columns wn*TN + qn*TN/2 .. of the tile
-    const int c0 = wn * TN + qn * (TN / 2);
-    const u16* sb = (const u16*)(smem + 2 * CV_PATCH_B + st * B_B + (c0 >> 7) * HALF);
+  auto readB = [&](int qn, int st) __attribute__((always_inline)) {   // columns wn*TN + qn*TN/2 .. of the tile
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
       for (int fn = 0; fn < QF; ++fn)
-        bf[qn][ks][fn] = *(const uint4*)(sb + lds_off((c0 & 127) + fn * 16 + frow, ks * 4 + fchunk));
+        bf[qn][ks][fn] = __builtin_bit_cast(uint4, *(lds_u4*)((lds_c*)(uintptr_t)bbase[ks] + st * B_B + (qn * (TN / 2) + fn * 16) * 128));
   };
   auto tick = [&]() -> unsigned long long {
     if constexpr ((ABL & 256) != 0) return __builtin_amdgcn_s_memtime();
@@ -167,16 +202,24 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
     const unsigned long long m1_ = tick();
     if constexpr ((ABL & 256) != 0) st_[8] += m1_ - m0_;
     if constexpr (ABL & 4) return;
+    // the ReLU prologue in place, once per fragment (its first use, qn = 0): no relu'd copies held
+    // beside the fragments, half the v_pk_max of a per-use ReLU
+    if constexpr (RELU && !(ABL & 32)) {
+      if (qn == 0) {
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          #pragma unroll
+          for (int fm = 0; fm < HQ; ++fm) af[ks][fm] = relu_pk16(af[ks][fm]);
+      }
+    }
     if constexpr ((ABL & 1536) == 0) __builtin_amdgcn_s_setprio(1);
     #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       #pragma unroll
       for (int fm = 0; fm < HQ; ++fm) {
-        uint4 a = af[ks][fm];
-        if constexpr (RELU && !(ABL & 32)) a = relu_pk16(a);
         #pragma unroll
         for (int fn = 0; fn < QF; ++fn)
-          acc[qm * HQ + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], a, acc[qm * HQ + fm][qn * QF + fn]);
+          acc[qm * HQ + fm][qn * QF + fn] = K_::mfma16(bf[qn][ks][fn], af[ks][fm], acc[qm * HQ + fm][qn * QF + fn]);
       }
     if constexpr ((ABL & 1536) == 0) __builtin_amdgcn_s_setprio(0);
     if constexpr ((ABL & 256) != 0) { __builtin_amdgcn_sched_barrier(0); st_[9] += tick() - m1_; }
@@ -206,30 +249,53 @@ __global__ void __launch_bounds__(512, 1) gemm_cv3_kernel(const GemmP p) {
   if constexpr ((ABL & 8) != 0) st_[1] = __builtin_amdgcn_s_memtime();
   if constexpr ((ABL & 512) != 0) { if (wave_u >= 4) __builtin_amdgcn_s_setprio(1); }
   if (wm == 1) bar();
-  for (int t = 0; t < KT; ++t) {
-    const int cb = t / 9, tap = t - cb * 9, ky = tap / 3, kx = tap - ky * 3;
-    const int pb = cb & 1, st = t & 1;
-    const bool np = tap == 0 && cb + 1 < CB;    // this step streams the next block's patch
-    const bool n2 = t + 2 < KT;
-    // two half-step phases (A rows qm, both column halves: 16 MFMAs per wave at BN 128, 32 at
-    // BN 256) instead of four quadrant phases -- half the barriers per step (head.0c 449 / 453
-    // -> 433 / 421 us, the 768^2 ResidualBlock convs 676 / 684 -> 642 / 629 us in-frame,
-    // profiles/r03af_cv3_bn128_2phase/, r03ag_cv3_2phase/).  Phase 0 reads the step's weights
-    // and streams the next block's patch (its buffer was last read one phase earlier by the
-    // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
-    // phase 0), waits for step t+1, then issues the second weight half.
-    readA(0, pb, ky, kx); readB(0, st); readB(1, st);
-    if (np && !(ABL & 2) && !(ABL & 128)) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, PPW / 2); }
-    bar(); mma(0, 0); mma(0, 1); bar();
-    readA(1, pb, ky, kx);
-    if (n2 && !(ABL & 2) && !(ABL & 64)) issue_b(0, t + 2);
-    const unsigned long long v0_ = tick();
-    if (np) { if (n2) wait_vmcnt<PPW + 2>(); else wait_vmcnt<PPW>(); }
-    else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
-    if constexpr ((ABL & 256) != 0) st_[6] += tick() - v0_;
-    if (NBH == 2 && n2 && !(ABL & 2) && !(ABL & 64)) issue_b(1, t + 2);
-    bar(); mma(1, 0); mma(1, 1); bar();
+  // one channel block cb: its 9 taps unrolled (ky, kx and the weight stage of each step constant:
+  // step t = 9 cb + tap is in stage t & 1 = (cb + tap) & 1, ST0 = cb & 1)
+  int cb = 0;
+  auto block = [&](auto st0_tag) __attribute__((always_inline)) {
+    constexpr int ST0 = decltype(st0_tag)::value;
+    constexpr int pb = ST0;                       // (cb & 1 = cb * 9 & 1)
+    const bool nb = cb + 1 < CB;
+    #pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - ky * 3, st = (ST0 + tap) & 1;
+      const int t = cb * 9 + tap;
+      const bool np = tap == 0 && nb;             // this step streams the next block's patch
+      const bool n2 = t + 2 < KT;
+      // two half-step phases (A rows qm, both column halves: 16 MFMAs per wave at BN 128, 32 at
+      // BN 256) instead of four quadrant phases -- half the barriers per step (head.0c 449 / 453
+      // -> 433 / 421 us, the 768^2 ResidualBlock convs 676 / 684 -> 642 / 629 us in-frame,
+      // profiles/r03af_cv3_bn128_2phase/, r03ag_cv3_2phase/).  Phase 0 reads the step's weights
+      // and streams the next block's patch (its buffer was last read one phase earlier by the
+      // wave row behind); phase 1 streams weight step t+2 into this step's stage (read in
+      // phase 0), waits for step t+1, then issues the second weight half.
+      readA(0, ky, kx, pb); readB(0, st); readB(1, st);
+      if (np && !(ABL & 2) && !(ABL & 128)) { issue_patch3(cb + 1, pb ^ 1, 0); issue_patch3(cb + 1, pb ^ 1, PPW / 2); }
+      bar(); mma(0, 0); mma(0, 1); bar();
+      readA(1, ky, kx, pb);
+      if (n2 && !(ABL & 2) && !(ABL & 64)) issue_b(0, t + 2);
+      const unsigned long long v0_ = tick();
+      if (np) { if (n2) wait_vmcnt<PPW + 2>(); else wait_vmcnt<PPW>(); }
+      else { if (n2) wait_vmcnt<2>(); else wait_vmcnt<0>(); }
+      if constexpr ((ABL & 256) != 0) st_[6] += tick() - v0_;
+      if (NBH == 2 && n2 && !(ABL & 2) && !(ABL & 64)) issue_b(1, t + 2);
+      bar(); mma(1, 0); mma(1, 1); bar();
+    }
+    // the next block reads the other patch buffer
+    if constexpr (!TIGHT) {
+      const uint32_t d = pb ? (uint32_t)-CV_PATCH_B : (uint32_t)CV_PATCH_B;
+      #pragma unroll
+      for (int v = 0; v < 8; ++v)
+        #pragma unroll
+        for (int ks = 0; ks < 2; ++ks) abase[v][ks] += d;
+    }
+    ++cb;
+  };
+  for (int pair = 0; pair < CB / 2; ++pair) {
+    block(std::integral_constant<int, 0>{});
+    block(std::integral_constant<int, 1>{});
   }
+  if (CB & 1) block(std::integral_constant<int, 0>{});
   if (wm == 0) bar();
   if constexpr ((ABL & 512) != 0) __builtin_amdgcn_s_setprio(0);
 
@@ -389,7 +455,8 @@ int launch_cv3(const GemmP& p0, hipStream_t s, int th) {
       S % CV_TW || S % th || p.in_c % 64 || p.M % (S * S) || p.row_group || (p.head_w && p.store_mode != DP_STORE_HEAD_PS) ||
       p.gamma || p.pos || p.accumulate || (p.act != DP_ACT_NONE && p.act != DP_ACT_RELU))
     return DP_ERR_ARG;
-  if ((long long)p.M * p.in_c >= (1LL << 31) || (long long)p.N * p.ldb >= (1LL << 31)) return DP_ERR_ARG;
+  // (the input map < 2 GiB: the patch DMA's padding offset lies past it; weight byte offsets < 2^32)
+  if ((long long)p.M * p.in_c >= (1LL << 30) || (long long)p.N * p.ldb >= (1LL << 31)) return DP_ERR_ARG;
   int epi, bn;
   if (p.store_mode == DP_STORE_HEAD_PS) {
     if (p.N != 128 || !p.head_w || !p.head_corr || p.c_dtype != DP_F32 || p.R1 || p.R2 || p.act) return DP_ERR_ARG;

@@ -156,6 +156,10 @@ __device__ unsigned long long g_stamps[5 * 65536];
     __builtin_amdgcn_sched_barrier(0);                                                \
   } while (0)
 #define DP_STAMPS_DECL unsigned long long st0_ = 0, st1_ = 0, st2_ = 0, st3_ = 0
+// the persistent 8-phase engine: per workgroup and tile (up to P8_STAMP_TILES) [K loop start, K loop
+// done (boundary issue + epilogue begin), epilogue done (its stores issued)], + hw_id | xcc_id << 32
+constexpr int P8_STAMP_TILES = 8, P8_STAMP_W = 3 * P8_STAMP_TILES + 1;
+__device__ unsigned long long g_p8_stamps[P8_STAMP_W * 1024];
 #define DP_STAMP_SAVE(wg)                                                             \
   do {                                                                                \
     if (threadIdx.x == 0 && (wg) < 65536) {                                           \
@@ -1032,6 +1036,41 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
       : "=&s"(keep)
       : "v"(src), "s"(lds_dst)
       : "memory");
+}
+
+// The same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset (saddr form):
+// a K step's addresses are one scalar add away from the last step's, no per-lane 64-bit arithmetic.
+__device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_dst)
+      : "memory");
+}
+
+// The same through a buffer resource (4 SGPRs: base, num_records = bytes, raw): a lane whose byte
+// offset is past the buffer's end reads zeros -- the implicit conv's zero padding without a second
+// (zero page) address per lane.
+__device__ __forceinline__ void glds16b(uint32_t voff, u32x4_t rsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_dst)
+      : "memory");
+}
+// Raw buffer resource of `bytes` bytes at p (stride 0): the SGPR words of glds16b's rsrc.
+__device__ __forceinline__ u32x4_t raw_rsrc(const void* p, uint32_t bytes) {
+  const unsigned long long a = (unsigned long long)(uintptr_t)p;
+  u32x4_t r;
+  r.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu);
+  r.z = __builtin_amdgcn_readfirstlane(bytes);
+  r.w = 0x00020000u;
+  return r;
 }
 
 // LDS image of one operand tile: rows of BKT 16-bit elements (64 or 128 B), the
@@ -2271,9 +2310,18 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     bar();
     ++s;
   };
+#ifdef DP_STAMPS
+  unsigned long long p8st_[3 * P8_STAMP_TILES] = {};
+#endif
   for (int i = 0;; ++i) {
+#ifdef DP_STAMPS
+    if (i < P8_STAMP_TILES) DP_STAMP(p8st_[3 * i]);
+#endif
     step(i, 0, std::true_type{});
     for (int k = 1; k < KT; ++k) step(i, k, std::false_type{});
+#ifdef DP_STAMPS
+    if (i < P8_STAMP_TILES) DP_STAMP(p8st_[3 * i + 1]);
+#endif
     // tile boundary: the next tile's second A K tile goes out before the epilogue's stores
     // (its buffer's last reads were this step's phases 0 / 2, two barriers back)
     if (t_nxt >= 0) {
@@ -2286,11 +2334,24 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     const char* rstat = smem + RING + 8 * SLAB + (wm * 8 + (i & 1)) * CST + 512;   // wave group's row stats
     epilogue_mfma_buf<K_, ACT, HG, DCV, LNC>(p, acc, slab, cst, lane, tm * 256 + wm * TM, tn * 256 + wn * TN, crs,
                                              rstat);
+#ifdef DP_STAMPS
+    if (i < P8_STAMP_TILES) DP_STAMP(p8st_[3 * i + 2]);
+#endif
     if (t_nxt < 0) break;
     t_cur = t_nxt;
     t_nxt = next_tile(t_cur);
   }
   if (wm == 0) bar();
+#ifdef DP_STAMPS
+  if (threadIdx.x == 0 && wgid < 1024) {
+    unsigned hw_, xcc_;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));
+    unsigned long long* d_ = g_p8_stamps + P8_STAMP_W * wgid;
+    for (int j = 0; j < 3 * P8_STAMP_TILES; ++j) d_[j] = p8st_[j];
+    d_[3 * P8_STAMP_TILES] = hw_ | ((unsigned long long)xcc_ << 32);
+  }
+#endif
 }
 
 // (rstd, -rstd * mean) of a row from its 8 chunk statistics (K = 1024; Chan's merge, as
