@@ -2154,7 +2154,10 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   // successor in the walk: up to two tiles ahead of the one computed at KT = 2).  32-bit
   // element offsets of this lane's rows (host: M * lda, N * ldb < 2^31).
   int sa = 0, ta = t_cur, ka = 0, sb = 0, tb = t_cur, kb = 0;
-  int aoff[2][2], boff[2][2];
+  // byte offsets of this lane's rows from the K step's scalar base (p.A + 64 ka, p.B + 64 kb): the
+  // DMA is issued in the saddr form, no per-lane 64-bit address arithmetic per K step (host: M * lda,
+  // N * ldb < 2^31 elements)
+  uint32_t aoff[2][2], boff[2][2];
   auto a_tile = [&](int t) {
     int tm, tn;
     tile_coords(p, t, tm, tn);
@@ -2163,7 +2166,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
       #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int m = tm * 256 + 128 * h + j * 64 + prow;
-        aoff[h][j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
+        aoff[h][j] = 2u * (uint32_t)((m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8);
       }
   };
   auto b_tile = [&](int t) {
@@ -2172,12 +2175,12 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
     #pragma unroll
     for (int h = 0; h < 2; ++h)
       #pragma unroll
-      for (int j = 0; j < 2; ++j) boff[h][j] = (tn * 256 + 128 * h + j * 64 + prow) * (int)p.ldb + pchunk * 8;
+      for (int j = 0; j < 2; ++j) boff[h][j] = 2u * (uint32_t)((tn * 256 + 128 * h + j * 64 + prow) * (int)p.ldb + pchunk * 8);
   };
   auto issueA = [&](int h) {   // A half h of step sa -> buffer sa & 1
     const uint32_t dst = lds_base + (sa & 1) * TILEB + h * HALF;
     #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(p.A + (aoff[h][j] + ka * 64), dst + j * 8192);
+    for (int j = 0; j < 2; ++j) glds16s(aoff[h][j], p.A + ka * 64, dst + j * 8192);
   };
   auto nextA = [&]() {
     ++sa;
@@ -2190,7 +2193,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   auto issueB = [&](int h) {
     const uint32_t dst = lds_base + (sb & 1) * TILEB + (2 + h) * HALF;
     #pragma unroll
-    for (int j = 0; j < 2; ++j) glds16(p.B + (boff[h][j] + kb * 64), dst + j * 8192);
+    for (int j = 0; j < 2; ++j) glds16s(boff[h][j], p.B + kb * 64, dst + j * 8192);
   };
   auto nextB = [&]() {
     ++sb;
@@ -2203,21 +2206,49 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   f32x4_t acc[8][4];
   const int frow = lane & 15, fchunk = lane >> 4;
   uint4 af[2][4], bf[2][2][2];
-  auto readA = [&](int qm, int buf) {
-    const u16* sa_ = (const u16*)(smem + buf * TILEB + wm * HALF);
+  // fragment addresses: per-lane bases per (buffer, ks) + compile-time ds_read immediates -- a
+  // fragment row r = q 64 / 32 + f 16 + frow has r & 7 = frow & 7, so its swizzled chunk is lane-fixed;
+  // the K loop below is unrolled by the two buffers (KT even), so the base is a constant choice
+  typedef __attribute__((address_space(3))) const char lds_c;
+  typedef __attribute__((address_space(3))) const u32x4_t lds_u4;
+  uint32_t abase[2], bbase[2];   // buffer 0; buffer 1 sits TILEB above (64 KB: past the ds_read immediate)
+  {
+    const uint32_t l0 = lds_addr(smem);
     #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks) {
+      const uint32_t sw = (uint32_t)(((ks * 4 + fchunk) ^ (frow & 7)) << 4);
+      abase[ks] = l0 + wm * HALF + frow * 128 + sw;
+      bbase[ks] = l0 + (2 + (wn >> 1)) * HALF + ((wn & 1) * 64 + frow) * 128 + sw;
+    }
+  }
+  // the buffer as a std::integral_constant (unrolled loop) or a runtime int (odd KT); buffer 1's
+  // address is one add on a laundered base, so the compiler does not keep both in registers
+  auto pick = [](const uint32_t (&b)[2], auto buf, int ks) __attribute__((always_inline)) -> uint32_t {
+    uint32_t x = b[ks];
+    if constexpr (std::is_integral_v<decltype(buf)>) return x + (buf ? (uint32_t)TILEB : 0u);
+    else if constexpr (decltype(buf)::value == 0) return x;
+    else {
+      asm volatile("" : "+v"(x));
+      return x + (uint32_t)TILEB;
+    }
+  };
+  auto readA = [&](int qm, auto buf) __attribute__((always_inline)) {
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      lds_c* base = (lds_c*)(uintptr_t)pick(abase, buf, ks);
       #pragma unroll
       for (int fm = 0; fm < 4; ++fm)
-        af[ks][fm] = *(const uint4*)(sa_ + lds_off(qm * 64 + fm * 16 + frow, ks * 4 + fchunk));
+        af[ks][fm] = __builtin_bit_cast(uint4, *(lds_u4*)(base + (qm * 64 + fm * 16) * 128));
+    }
   };
-  auto readB = [&](int qn, int buf) {
-    const u16* sb_ = (const u16*)(smem + buf * TILEB + (2 + (wn >> 1)) * HALF);
+  auto readB = [&](int qn, auto buf) __attribute__((always_inline)) {
     #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks) {
+      lds_c* base = (lds_c*)(uintptr_t)pick(bbase, buf, ks);
       #pragma unroll
       for (int fn = 0; fn < 2; ++fn)
-        bf[qn][ks][fn] = *(const uint4*)(sb_ + lds_off((wn & 1) * 64 + qn * 32 + fn * 16 + frow, ks * 4 + fchunk));
+        bf[qn][ks][fn] = __builtin_bit_cast(uint4, *(lds_u4*)(base + (qn * 32 + fn * 16) * 128));
+    }
   };
   // FIRST: a tile's first K step -- its ks = 0 MFMAs start from a zero accumulator (no
   // per-tile clearing of the 128 accumulator registers)
@@ -2281,8 +2312,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
   int s = 0;
   // one K step s (k-th of the i-th tile): the 8-phase schedule of gemm_8ph_kernel with the
   // issue cursors deciding what streams in
-  auto step = [&](int i, int k, auto first) {
-    const int buf = s & 1;
+  auto step = [&](int i, int k, auto first, auto buf) __attribute__((always_inline)) {
     const bool a1 = sa == s + 1 && ta >= 0;   // step s+1's A not issued yet (it was at a boundary)
     const bool b2 = tb >= 0;                  // sb == s + 2
     // phase 0: quadrant (0,0)
@@ -2317,8 +2347,20 @@ __global__ void __launch_bounds__(512, 1) gemm_p8ph_kernel(const GemmP p) {
 #ifdef DP_STAMPS
     if (i < P8_STAMP_TILES) DP_STAMP(p8st_[3 * i]);
 #endif
-    step(i, 0, std::true_type{});
-    for (int k = 1; k < KT; ++k) step(i, k, std::false_type{});
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    if ((KT & 1) == 0) {   // step s = i KT + k is in buffer k & 1
+      step(i, 0, std::true_type{}, B0{});
+      int k = 1;
+      for (; k + 1 < KT; k += 2) {
+        step(i, k, std::false_type{}, B1{});
+        step(i, k + 1, std::false_type{}, B0{});
+      }
+      step(i, k, std::false_type{}, B1{});
+    } else {
+      step(i, 0, std::true_type{}, s & 1);
+      for (int k = 1; k < KT; ++k) step(i, k, std::false_type{}, s & 1);
+    }
 #ifdef DP_STAMPS
     if (i < P8_STAMP_TILES) DP_STAMP(p8st_[3 * i + 1]);
 #endif

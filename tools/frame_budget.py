@@ -56,6 +56,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--md")
+    ap.add_argument("--alone-md", help="per-kernel alone times (average over the serial frames) as markdown")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     # frames = runs of launches from one patchify launch to the next; only frames whose launches never
@@ -71,6 +72,7 @@ def main():
         if cur is not None:
             cur.append(r)
     tot = defaultdict(float)
+    per = defaultdict(lambda: [0, 0.0])       # (kernel, workgroups) -> [launches, us] over the serial frames
     frames = skipped = 0
     spans = sorted(max(r[1] for r in g) - g[0][0] for g in groups)
     med = spans[len(spans) // 2]
@@ -95,6 +97,9 @@ def main():
         frames += 1
         for t0, t1, name, wgs in g:
             tot[classify(name, wgs)] += (t1 - t0) * 1e-3
+            k = per[(re.sub(r"\(anonymous namespace\)::", "", name).split("(")[0], wgs)]
+            k[0] += 1
+            k[1] += (t1 - t0) * 1e-3
     if frames == 0:
         raise SystemExit("no serial frame in the trace (every frame's launches overlap)")
     flop = dict(PATCH)
@@ -130,6 +135,17 @@ def main():
     print(out)
     if a.md:
         open(a.md, "w").write(out + "\n")
+    if a.alone_md:
+        al = [f"Per-kernel ALONE times: the {frames} serial frames of `{a.trace.split('/')[-1]}` (every launch on one "
+              f"stream, so each ran alone on the chip); kernel, workgroups, launches per frame, average us per launch, "
+              f"us per frame", "", "| kernel | workgroups | launches / frame | avg us | us / frame | phase |",
+              "|---|---:|---:|---:|---:|---|"]
+        for (name, wgs), (n, us) in sorted(per.items(), key=lambda kv: -kv[1][1]):
+            if us / frames < 5.0:
+                continue
+            al.append(f"| `{name[:90]}` | {wgs} | {n / frames:g} | {us / n:.2f} | {us / frames:.1f} | "
+                      f"{classify(name, wgs)} |")
+        open(a.alone_md, "w").write("\n".join(al) + "\n")
 
 
 if __name__ == "__main__":

@@ -18,6 +18,9 @@ sys.path.insert(0, os.path.join(REPO, "ml-depth-pro-video_amd"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=2)
+    ap.add_argument("--serial", action="store_true",
+                    help="every launch on one stream (Engine.serial_side): each launch alone on the chip -- "
+                         "the frames tools/frame_budget.py sums and takes per-kernel alone times from")
     args = ap.parse_args()
     from depth_pro import ops
     from depth_pro.depth_pro import _compute_dtype
@@ -28,6 +31,7 @@ def main():
     code = _compute_dtype(torch.float32)
     eng = Engine(pack_weights(synthetic_state_dict(0), dev, code), dev, code)
     img = torch.from_numpy(np.random.default_rng(0).integers(0, 256, (1536, 1536, 3), dtype=np.uint8)).to(dev)
+    eng.serial_side = args.serial
     for _ in range(args.frames):
         ops.normalize_u8(img, eng.x0)
         eng.forward()
