@@ -2545,21 +2545,23 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
 
   // LDS-DMA pieces: 8 rows x 128 B per wave, the 16-B chunk swizzled on the source address
   const int pchunk = (lane & 7) ^ ((lane >> 3) & 7);
-  int aoff[5];
+  // byte offsets of this lane's rows from the step's scalar base (saddr DMA; the planner's off32:
+  // M * lda, N * ldb < 2^31 elements)
+  uint32_t aoff[5];
   #pragma unroll
   for (int j = 0; j < 5; ++j) {
     const int m = m0 + j * 64 + wave * 8 + (lane >> 3);
-    aoff[j] = (m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8;
+    aoff[j] = 2u * (uint32_t)((m < p.M ? m : p.M - 1) * (int)p.lda + pchunk * 8);
   }
   // B quarter q = output columns {q*32 .. +31} u {128 + q*32 .. +31}: waves 0-3 / 4-7 take 8 rows each
   const int brow0 = wave_u < 4 ? wave_u * 8 : 128 + (wave_u - 4) * 8;   // + q * 32
-  const int boff = (n0 + brow0 + (lane >> 3)) * (int)p.ldb + pchunk * 8;
+  const uint32_t boff = 2u * (uint32_t)((n0 + brow0 + (lane >> 3)) * (int)p.ldb + pchunk * 8);
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   auto issueA = [&](int j, int t) {
-    glds16(p.A + (aoff[j] + t * 64), lds0 + (t & 1) * BUF + j * 8192 + wave_u * 1024);
+    glds16s(aoff[j], p.A + t * 64, lds0 + (t & 1) * BUF + j * 8192 + wave_u * 1024);
   };
   auto issueB = [&](int q, int t) {
-    glds16(p.B + (boff + q * 32 * (int)p.ldb + t * 64), lds0 + (t & 1) * BUF + A_BYTES + (brow0 + q * 32) * 128);
+    glds16s(boff, p.B + (q * 32 * (int)p.ldb + t * 64), lds0 + (t & 1) * BUF + A_BYTES + (brow0 + q * 32) * 128);
   };
 
   f32x4_t acc[FM][FN];
@@ -2569,21 +2571,43 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int frow = lane & 15, fchunk = lane >> 4;
   uint4 af[2][FM], bf[2][2];
-  auto readA = [&](int buf) {
-    const u16* sa = (const u16*)(smem + buf * BUF);
-    #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      #pragma unroll
-      for (int fm = 0; fm < FM; ++fm)
-        af[ks][fm] = *(const uint4*)(sa + lds_off(wm * TM + fm * 16 + frow, ks * 4 + fchunk));
+  // fragment addresses: per-lane bases (buffer 0) per ks + ds_read immediates -- fragment row r =
+  // 16 f + frow (+ 80 wm / 32 q) has r & 7 = frow & 7, so its swizzled chunk is lane-fixed.  Buffer 1
+  // sits BUF (72 KiB) above, past the 16-bit immediate: one add on a laundered base (the compiler
+  // would otherwise keep all four bases live across the loop)
+  typedef __attribute__((address_space(3))) const char lds_c;
+  typedef __attribute__((address_space(3))) const u32x4_t lds_u4;
+  uint32_t abase[2], bbase[2];
+  #pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const uint32_t sw = (uint32_t)(((ks * 4 + fchunk) ^ (frow & 7)) << 4);
+    abase[ks] = lds0 + (wm * TM + frow) * 128 + sw;
+    bbase[ks] = lds0 + A_BYTES + (wn * TN + frow) * 128 + sw;
+  }
+  auto pick = [](const uint32_t (&b)[2], auto buf, int ks) __attribute__((always_inline)) -> uint32_t {
+    uint32_t x = b[ks];
+    if constexpr (std::is_integral_v<decltype(buf)>) return x + (buf ? (uint32_t)BUF : 0u);
+    else if constexpr (decltype(buf)::value == 0) return x;
+    else {
+      asm volatile("" : "+v"(x));
+      return x + (uint32_t)BUF;
+    }
   };
-  auto readB = [&](int q, int buf) {
-    const u16* sb = (const u16*)(smem + buf * BUF + A_BYTES);
+  auto readA = [&](auto buf) __attribute__((always_inline)) {
     #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks) {
+      lds_c* base = (lds_c*)(uintptr_t)pick(abase, buf, ks);
       #pragma unroll
-      for (int f = 0; f < 2; ++f)
-        bf[ks][f] = *(const uint4*)(sb + lds_off(wn * TN + q * 32 + f * 16 + frow, ks * 4 + fchunk));
+      for (int fm = 0; fm < FM; ++fm) af[ks][fm] = __builtin_bit_cast(uint4, *(lds_u4*)(base + fm * 16 * 128));
+    }
+  };
+  auto readB = [&](int q, auto buf) __attribute__((always_inline)) {
+    #pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      lds_c* base = (lds_c*)(uintptr_t)pick(bbase, buf, ks);
+      #pragma unroll
+      for (int f = 0; f < 2; ++f) bf[ks][f] = __builtin_bit_cast(uint4, *(lds_u4*)(base + (q * 32 + f * 16) * 128));
+    }
   };
   auto mma = [&](int q) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2613,8 +2637,9 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
   if (KT > 1) wait_vmcnt<8>(); else wait_vmcnt<3>();
   lds_barrier();
   if (wave >= 4) bar();
-  for (int s = 0; s < KT; ++s) {
-    const int buf = s & 1;
+  // one K step s in buffer buf (a std::integral_constant when the loop below is unrolled by the
+  // two buffers -- KT even -- else s & 1)
+  auto step = [&](int s, auto buf) __attribute__((always_inline)) {
     const bool a1 = s + 1 < KT, a2 = s + 2 < KT;
     // phase 0: A fragments + B quarter 0; retire Bq1(s) (younger: 2 + 6 a1)
     readA(buf); readB(0, buf);
@@ -2638,6 +2663,14 @@ __global__ void __launch_bounds__(512, 1) gemm_8ph320_kernel(const GemmP p) {
     if (a2) { issueA(3, s + 2); issueA(4, s + 2); }
     if (a2) wait_vmcnt<8>(); else if (a1) wait_vmcnt<3>();
     bar(); mma(3); bar();
+  };
+  if ((KT & 1) == 0) {
+    for (int s = 0; s < KT; s += 2) {
+      step(s, std::integral_constant<int, 0>{});
+      step(s + 1, std::integral_constant<int, 1>{});
+    }
+  } else {
+    for (int s = 0; s < KT; ++s) step(s, s & 1);
   }
   if (wave < 4) bar();
   if (p.dbg & 1) {   // ablation (tools/gemm_bench.py --ablate): no epilogue
