@@ -58,7 +58,18 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     M, K = 20195, 1024
     ws = ops.gemm_workspace(dev)
-    for name, N, act in (("fc1 (LN + GELU)", 4096, DP_ACT_GELU), ("qkv (LN)", 3072, 0)):
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--more", action="store_true",
+                    help="also the fc1 shape without GELU, the qkv shape with it, and fc1 on 8- / 2-row tile bands")
+    args = ap.parse_args()
+    runs = [("fc1 (LN + GELU)", 4096, DP_ACT_GELU, 0), ("qkv (LN)", 3072, 0, 0)]
+    if args.more:
+        runs += [("fc1 shape, no GELU", 4096, 0, 0), ("qkv shape + GELU", 3072, DP_ACT_GELU, 0),
+                 ("fc1, 8-row bands", 4096, DP_ACT_GELU, 1 << 18), ("fc1, 2-row bands", 4096, DP_ACT_GELU, 1 << 19)]
+    for name, N, act, dbg in runs:
+        lib.dp_gemm_debug_flags(dbg)
         A = torch.randn(M, K, device=dev, generator=g).to(dt)
         B = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(dt)
         bias = torch.randn(N, device=dev, generator=g)
@@ -81,7 +92,8 @@ def main():
         assert fn(st.ctypes.data, wgs) == 0
         T = ((M + 255) // 256) * (N // 256)
         ntiles = np.array([(T - w + wgs - 1) // wgs for w in range(wgs)])
-        print(f"{name:16s} {ms * 1e3:7.1f} us/launch (stamped build) | {analyse(st, ntiles)}", flush=True)
+        print(f"{name:20s} {ms * 1e3:7.1f} us/launch (stamped build) | {analyse(st, ntiles)}", flush=True)
+    lib.dp_gemm_debug_flags(0)
 
 
 if __name__ == "__main__":
