@@ -2,7 +2,7 @@
 # One bounded GPU session (run on the gpurun box from the repo root):
 #   GPU tests -> bench line -> rocprofv3 kernel-trace stats -> FETCH/WRITE PMC passes.
 # Every GPU step has its own time limit; the first failure ends the script.
-# Usage: tools/gpu_check.sh <tag> [tests|smoke|bench|prof|pmc|sq ...]   (default: tests bench prof pmc)
+# Usage: tools/gpu_check.sh <tag> [tests|smoke|bench|prof|pmc|sq|serial|side|loop ...]   (default: tests bench prof pmc)
 set -eo pipefail
 TAG=${1:-r01}
 shift || true
@@ -49,6 +49,12 @@ for S in $STEPS; do
       # fc1 on the three engines that can run it, same box
       timeout -k 10 300 python -u tools/gemm_bench.py --tile 8ph256x256,p8ph256x256,8ph320x256 --only fc1 --ablate \
         > $OUT/gemm_fc1_engines.txt 2>&1 ;;
+    serial)
+      # serial frames (every launch alone on the chip): the per-frame budget and per-kernel alone times
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_serial -o prof --output-format csv \
+        -- python3 tools/frame_once.py --frames 5 --serial > $OUT/prof_serial.log 2>&1
+      python3 tools/frame_budget.py $OUT/prof_serial/prof_kernel_trace.csv --md $OUT/frame_budget.md \
+        --alone-md $OUT/kernel_alone.md > /dev/null ;;
     side)
       # side-encoder cost by ablation (DP_ABLATE=side: image / FOV encoders skipped) vs the full frame
       DP_ABLATE=side timeout -k 10 300 python -u bench.py --ab --no-cpu-baseline --steps 40 > $OUT/bench_noside.json 2> $OUT/bench_noside.err
