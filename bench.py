@@ -51,7 +51,7 @@ def tile_kernel(tile: int, dtype: torch.dtype) -> str:
 
 # The PMC traffic summary the bench line cites (tools/pmc_traffic.py over separate FETCH_SIZE /
 # WRITE_SIZE passes of the tree being benched); named explicitly, updated with each profiled tree.
-PMC_TRAFFIC = "profiles/r05_pmc_traffic.json"
+PMC_TRAFFIC = "profiles/r06_pmc_traffic.json"
 
 
 def pmc_traffic(kernel: str, workgroups: int):
@@ -73,7 +73,7 @@ def pmc_traffic(kernel: str, workgroups: int):
 # copied from gpurun_out/): the dominant kernel's average duration there (every launch of it in that run:
 # graph replays, where it overlaps other streams, and the instrumented frames) is reported beside the live
 # HIP-event figure, so the line's roofline fraction can be checked against the committed profile.
-PROF_STATS = "profiles/r05_kernel_stats.csv"
+PROF_STATS = "profiles/r06_kernel_stats.csv"
 
 
 def rocprof_avg_us(kernel: str):
