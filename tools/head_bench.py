@@ -52,6 +52,16 @@ def main():
                        ("head.ps (composed deconv + conv + 1x1)", f1, 2.0 * S * S * 128 * 1152)):
         us = timeit(f)
         print(f"{lab:40s} {us:7.1f} us  {fl / us / 1e6:6.1f} TF", flush=True)
+    if "--ablate" in sys.argv:
+        # the big engine's timing ablations (dp_gemm_debug_flags; results are wrong): what bounds head.ps
+        from depth_pro import _lib
+        lib = _lib.load()
+        for lab, dbg in (("no epilogue", 1), ("no loads in the K loop", 2), ("no MFMA (one fragment read)", 4),
+                         ("no loads, no epilogue", 3)):
+            lib.dp_gemm_debug_flags(dbg)
+            us = timeit(f1)
+            lib.dp_gemm_debug_flags(0)
+            print(f"head.ps, {lab:34s} {us:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
